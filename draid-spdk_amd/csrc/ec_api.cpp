@@ -1,0 +1,357 @@
+// ec_api.cpp -- extern "C" boundary of libdraid_ec.so (declared in
+// include/draid_ec.h).  Argument checking follows isa-l v2.30's raid.h /
+// gf_vect_mul.h contracts (the functions the reference binds at
+// module/bdev/raid/raid5.c:189-201, raid5_simple.c:131-135 and
+// examples/bdev/gf_vect_mul/gf_vect_mul.c:40-49,101,108); the arithmetic runs in
+// the HIP kernels of ec_kernels.hip.  There is no CPU fallback: when no GPU is
+// usable every compute entry point fails with a negative code.
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/draid_ec.h"
+#include "ec_gf.hpp"
+#include "ec_launch.hpp"
+
+using draid::ArgPtrTable;
+using draid::kMaxArgPtrs;
+
+namespace {
+
+thread_local char t_err[256] = "";
+
+int fail_hip(hipError_t e, const char* what)
+{
+    snprintf(t_err, sizeof(t_err), "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
+    return -static_cast<int>(e == hipSuccess ? 1 : e);
+}
+
+int fail_arg(const char* what)
+{
+    snprintf(t_err, sizeof(t_err), "invalid argument: %s", what);
+    return 1;
+}
+
+hipStream_t sync_stream() { return hipStreamPerThread; }
+
+// Per-thread device scratch: a pointer table for calls with more vectors than
+// fit in kernel arguments, and a 4-byte flag for the *_check calls.
+struct Scratch {
+    void* table = nullptr;
+    size_t table_bytes = 0;
+    uint32_t* flag = nullptr;
+    ~Scratch()
+    {
+        if (table)
+            (void)hipFree(table);
+        if (flag)
+            (void)hipFree(flag);
+    }
+};
+thread_local Scratch t_scratch;
+
+// Makes the pointers of one stripe available to a kernel: in kernel arguments
+// when they fit, else in the per-thread device table.
+int stage_pointers(void** array, int n, ArgPtrTable* args, const uint8_t* const** table)
+{
+    *table = nullptr;
+    if (n <= kMaxArgPtrs) {
+        memset(args, 0, sizeof(*args));
+        for (int i = 0; i < n; ++i)
+            args->p[i] = static_cast<const uint8_t*>(array[i]);
+        return 0;
+    }
+    const size_t bytes = sizeof(void*) * static_cast<size_t>(n);
+    if (t_scratch.table_bytes < bytes) {
+        if (t_scratch.table)
+            (void)hipFree(t_scratch.table);
+        t_scratch.table = nullptr;
+        t_scratch.table_bytes = 0;
+        hipError_t e = hipMalloc(&t_scratch.table, bytes);
+        if (e != hipSuccess)
+            return fail_hip(e, "hipMalloc(pointer table)");
+        t_scratch.table_bytes = bytes;
+    }
+    hipError_t e = hipMemcpyAsync(t_scratch.table, array, bytes, hipMemcpyHostToDevice,
+                                  sync_stream());
+    if (e != hipSuccess)
+        return fail_hip(e, "hipMemcpyAsync(pointer table)");
+    *table = static_cast<const uint8_t* const*>(t_scratch.table);
+    return 0;
+}
+
+int finish_sync(hipError_t e, const char* what)
+{
+    if (e != hipSuccess)
+        return fail_hip(e, what);
+    e = hipStreamSynchronize(sync_stream());
+    if (e != hipSuccess)
+        return fail_hip(e, "hipStreamSynchronize");
+    return 0;
+}
+
+int encode_one(uint32_t k, uint32_t m, int len, void** array)
+{
+    ArgPtrTable args;
+    const uint8_t* const* table;
+    int rc = stage_pointers(array, static_cast<int>(k + m), &args, &table);
+    if (rc)
+        return rc;
+    return finish_sync(draid::launch_encode(k, m, static_cast<uint64_t>(len), 1, table,
+                                            table ? nullptr : &args, sync_stream()),
+                       "launch_encode");
+}
+
+int check_one(uint32_t k, uint32_t m, int len, void** array)
+{
+    if (!t_scratch.flag) {
+        hipError_t e = hipMalloc(&t_scratch.flag, sizeof(uint32_t));
+        if (e != hipSuccess)
+            return fail_hip(e, "hipMalloc(flag)");
+    }
+    ArgPtrTable args;
+    const uint8_t* const* table;
+    int rc = stage_pointers(array, static_cast<int>(k + m), &args, &table);
+    if (rc)
+        return rc;
+    hipError_t e = hipMemsetAsync(t_scratch.flag, 0, sizeof(uint32_t), sync_stream());
+    if (e != hipSuccess)
+        return fail_hip(e, "hipMemsetAsync(flag)");
+    e = draid::launch_check(k, m, static_cast<uint64_t>(len), table, table ? nullptr : &args,
+                            t_scratch.flag, sync_stream());
+    if (e != hipSuccess)
+        return fail_hip(e, "launch_check");
+    uint32_t host_flag = 0;
+    e = hipMemcpyAsync(&host_flag, t_scratch.flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       sync_stream());
+    rc = finish_sync(e, "hipMemcpyAsync(flag)");
+    if (rc)
+        return rc;
+    return host_flag ? 1 : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------- isa-l shaped
+
+int draid_xor_gen(int vects, int len, void** array)
+{
+    if (vects < 3 || len < 0 || !array)
+        return fail_arg("xor_gen needs vects >= 3, len >= 0");
+    if (len == 0)
+        return 0;
+    return encode_one(static_cast<uint32_t>(vects - 1), 1, len, array);
+}
+
+int draid_pq_gen(int vects, int len, void** array)
+{
+    if (vects < 4 || len < 0 || (len & 31) || !array)
+        return fail_arg("pq_gen needs vects >= 4, len % 32 == 0");
+    if (len == 0)
+        return 0;
+    return encode_one(static_cast<uint32_t>(vects - 2), 2, len, array);
+}
+
+int draid_xor_check(int vects, int len, void** array)
+{
+    if (vects < 3 || len < 0 || !array)
+        return fail_arg("xor_check needs vects >= 3, len >= 0");
+    if (len == 0)
+        return 0;
+    return check_one(static_cast<uint32_t>(vects - 1), 1, len, array);
+}
+
+int draid_pq_check(int vects, int len, void** array)
+{
+    if (vects < 4 || len < 0 || (len & 31) || !array)
+        return fail_arg("pq_check needs vects >= 4, len % 32 == 0");
+    if (len == 0)
+        return 0;
+    return check_one(static_cast<uint32_t>(vects - 2), 2, len, array);
+}
+
+unsigned char draid_gf_mul(unsigned char a, unsigned char b) { return draid::gf_mul_host(a, b); }
+
+unsigned char draid_gf_inv(unsigned char a) { return draid::gf_inv_host(a); }
+
+void draid_gf_vect_mul_init(unsigned char c, unsigned char* tbl)
+{
+    for (int i = 0; i < 16; ++i) {
+        tbl[i] = draid::gf_mul_host(c, static_cast<uint8_t>(i));
+        tbl[16 + i] = draid::gf_mul_host(c, static_cast<uint8_t>(i << 4));
+    }
+}
+
+int draid_gf_vect_mul(int len, unsigned char* tbl, void* src, void* dest)
+{
+    if (len < 0 || (len & 31) || !tbl)
+        return fail_arg("gf_vect_mul needs len % 32 == 0");
+    if (len == 0)
+        return 0;
+    return finish_sync(draid::launch_gf_vect_mul(static_cast<uint64_t>(len), tbl,
+                                                 static_cast<const uint8_t*>(src),
+                                                 static_cast<uint8_t*>(dest), sync_stream()),
+                       "launch_gf_vect_mul");
+}
+
+int draid_recover(int k, int m, int len, void** array, int nfail, const int* fail)
+{
+    if (k < 1 || k > 255 || m < 1 || m > 2 || len < 0 || nfail < 0 || nfail > m || !array ||
+        (nfail && !fail))
+        return fail_arg("recover needs 1 <= k <= 255, m in {1,2}, nfail <= m");
+    uint8_t f[2] = {DRAID_EC_FAIL_NONE, DRAID_EC_FAIL_NONE};
+    for (int i = 0; i < nfail; ++i) {
+        if (fail[i] < 0 || fail[i] >= k + m)
+            return fail_arg("recover: failed index out of range");
+        if (i == 1 && fail[1] == fail[0])
+            return fail_arg("recover: duplicate failed index");
+        f[i] = static_cast<uint8_t>(fail[i]);
+    }
+    if (nfail == 0 || len == 0)
+        return 0;
+    ArgPtrTable args;
+    const uint8_t* const* table;
+    int rc = stage_pointers(array, k + m, &args, &table);
+    if (rc)
+        return rc;
+    return finish_sync(draid::launch_reconstruct(static_cast<uint32_t>(k), static_cast<uint32_t>(m),
+                                                 static_cast<uint64_t>(len), 1, table,
+                                                 table ? nullptr : &args, nullptr, f[0], f[1],
+                                                 sync_stream()),
+                       "launch_reconstruct");
+}
+
+// ---------------------------------------------------------------- batched
+
+static int check_batch(const draid_ec_stripe_batch* b)
+{
+    if (!b)
+        return fail_arg("batch is NULL");
+    if (b->k < 1 || b->k > 255 || b->m < 1 || b->m > 2 || b->flags != 0)
+        return fail_arg("batch needs 1 <= k <= 255, m in {1,2}, flags == 0");
+    if (b->nstripes && (!b->strips || b->strip_len == 0))
+        return b->strip_len == 0 ? 0 : fail_arg("batch strips table is NULL");
+    return 0;
+}
+
+int draid_ec_encode(const draid_ec_stripe_batch* b, void* stream)
+{
+    int rc = check_batch(b);
+    if (rc || !b->nstripes || !b->strip_len)
+        return rc;
+    hipError_t e = draid::launch_encode(b->k, b->m, b->strip_len, b->nstripes,
+                                        reinterpret_cast<const uint8_t* const*>(b->strips), nullptr,
+                                        static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail_hip(e, "launch_encode");
+}
+
+int draid_ec_reconstruct(const draid_ec_stripe_batch* b, const uint8_t* fail, void* stream)
+{
+    int rc = check_batch(b);
+    if (rc || !b->nstripes || !b->strip_len)
+        return rc;
+    if (!fail)
+        return fail_arg("reconstruct: fail table is NULL");
+    hipError_t e = draid::launch_reconstruct(
+        b->k, b->m, b->strip_len, b->nstripes, reinterpret_cast<const uint8_t* const*>(b->strips),
+        nullptr, fail, DRAID_EC_FAIL_NONE, DRAID_EC_FAIL_NONE, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail_hip(e, "launch_reconstruct");
+}
+
+// ---------------------------------------------------------------- runtime
+
+int draid_ec_abi_version(void) { return DRAID_EC_ABI_VERSION; }
+
+const char* draid_ec_last_error(void) { return t_err; }
+
+int draid_ec_set_device(int device)
+{
+    hipError_t e = hipSetDevice(device);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipSetDevice");
+}
+
+int draid_ec_device_count(int* count)
+{
+    hipError_t e = hipGetDeviceCount(count);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipGetDeviceCount");
+}
+
+int draid_ec_stream_create(void** stream)
+{
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess)
+        return fail_hip(e, "hipStreamCreateWithFlags");
+    *stream = s;
+    return 0;
+}
+
+int draid_ec_stream_destroy(void* stream)
+{
+    hipError_t e = hipStreamDestroy(static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail_hip(e, "hipStreamDestroy");
+}
+
+int draid_ec_stream_query(void* stream)
+{
+    hipError_t e = hipStreamQuery(static_cast<hipStream_t>(stream));
+    if (e == hipSuccess)
+        return 0;
+    if (e == hipErrorNotReady)
+        return 1;
+    return fail_hip(e, "hipStreamQuery");
+}
+
+int draid_ec_stream_synchronize(void* stream)
+{
+    hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail_hip(e, "hipStreamSynchronize");
+}
+
+int draid_ec_device_alloc(void** ptr, size_t bytes)
+{
+    hipError_t e = hipMalloc(ptr, bytes);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipMalloc");
+}
+
+int draid_ec_device_free(void* ptr)
+{
+    hipError_t e = hipFree(ptr);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipFree");
+}
+
+int draid_ec_host_register(void* ptr, size_t bytes)
+{
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipHostRegister");
+}
+
+int draid_ec_host_unregister(void* ptr)
+{
+    hipError_t e = hipHostUnregister(ptr);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipHostUnregister");
+}
+
+int draid_ec_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream)
+{
+    hipMemcpyKind k;
+    switch (kind) {
+    case 0: k = hipMemcpyHostToDevice; break;
+    case 1: k = hipMemcpyDeviceToHost; break;
+    case 2: k = hipMemcpyDeviceToDevice; break;
+    default: return fail_arg("memcpy kind must be 0, 1 or 2");
+    }
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, k, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail_hip(e, "hipMemcpyAsync");
+}
+
+// Test/bench hook (not in the public header): pick a kernel variant for A/B
+// comparisons inside one process.  0 = default (non-temporal), 1 = plain loads.
+void draid_ec_set_variant(int v) { draid::set_variant(v); }
+
+}  // extern "C"

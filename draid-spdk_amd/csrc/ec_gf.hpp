@@ -1,0 +1,131 @@
+// ec_gf.hpp -- GF(2^8) arithmetic for the MI355X erasure-coding engine.
+//
+// Field: GF(2^8) / x^8+x^4+x^3+x^2+1 (0x11D), generator 2 -- the field isa-l
+// v2.30 uses for pq_gen / gf_mul (reference call sites:
+// examples/bdev/gf_vect_mul/gf_vect_mul.c:60-66,101,267).
+//
+// Everything here is byte-parallel integer work on 32-bit VALU lanes: no MFMA.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace draid {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// exp[0..511] (exp[i] = 2^(i mod 255)) and log[0..255] (log[0] unused).
+struct GfTables {
+    uint8_t exp[512];
+    uint8_t log[256];
+};
+
+constexpr GfTables make_gf_tables()
+{
+    GfTables t{};
+    unsigned x = 1;
+    for (int i = 0; i < 255; ++i) {
+        t.exp[i] = static_cast<uint8_t>(x);
+        t.log[x] = static_cast<uint8_t>(i);
+        x <<= 1;
+        if (x & 0x100u)
+            x ^= 0x11Du;
+    }
+    for (int i = 255; i < 512; ++i)
+        t.exp[i] = t.exp[i - 255];
+    return t;
+}
+
+inline constexpr GfTables kGfHost = make_gf_tables();
+
+// ---- host-side scalar helpers (isa-l ec_base.c gf_mul / gf_inv semantics) ----
+inline uint8_t gf_mul_host(uint8_t a, uint8_t b)
+{
+    if (!a || !b)
+        return 0;
+    return kGfHost.exp[kGfHost.log[a] + kGfHost.log[b]];
+}
+inline uint8_t gf_inv_host(uint8_t a) { return a ? kGfHost.exp[255 - kGfHost.log[a]] : 0; }
+
+// ---- device: multiply every byte by 2 (SWAR, isa-l pq_gen_base word form) ----
+__device__ __forceinline__ uint32_t gf_mul2(uint32_t q)
+{
+    const uint32_t hi = q & 0x80808080u;
+    const uint32_t mask = (hi << 1) - (hi >> 7);  // 0xFF in every byte whose bit 7 is set
+    return ((q & 0x7f7f7f7fu) << 1) ^ (mask & 0x1d1d1d1du);
+}
+__device__ __forceinline__ u32x4 gf_mul2(u32x4 q)
+{
+    const u32x4 hi = q & 0x80808080u;
+    const u32x4 mask = (hi << 1) - (hi >> 7);
+    return ((q & 0x7f7f7f7fu) << 1) ^ (mask & 0x1d1d1d1du);
+}
+
+// ---- device: multiply by a constant c through isa-l's 32-byte nibble table ----
+// lo[w] byte b = c * (4w + b)         (tbl[0..15]  of gf_vect_mul_init)
+// hi[w] byte b = c * ((4w + b) << 4)  (tbl[16..31] of gf_vect_mul_init)
+// isa-l looks the nibbles up with pshufb; on CDNA4 two v_perm_b32 (8-entry byte
+// selects from a register pair) plus a bit-3 blend do the same in registers.
+struct NibTable {
+    uint32_t lo[4];
+    uint32_t hi[4];
+};
+
+__host__ __device__ __forceinline__ uint32_t mul2_byte(uint32_t c)
+{
+    return ((c << 1) ^ ((c & 0x80u) ? 0x1du : 0u)) & 0xffu;
+}
+
+__host__ __device__ inline NibTable make_nib_table(uint32_t c)
+{
+    uint32_t p[8];  // c * 2^i
+    p[0] = c & 0xffu;
+    for (int i = 1; i < 8; ++i)
+        p[i] = mul2_byte(p[i - 1]);
+    NibTable t{};
+    for (int w = 0; w < 4; ++w) {
+        uint32_t lo = 0, hi = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int n = 4 * w + b;
+            uint32_t vl = 0, vh = 0;
+            for (int bit = 0; bit < 4; ++bit) {
+                if (n & (1 << bit)) {
+                    vl ^= p[bit];
+                    vh ^= p[bit + 4];
+                }
+            }
+            lo |= vl << (8 * b);
+            hi |= vh << (8 * b);
+        }
+        t.lo[w] = lo;
+        t.hi[w] = hi;
+    }
+    return t;
+}
+
+// 16-entry byte table lookup of the nibble held in every byte of n.
+__device__ __forceinline__ uint32_t lut16(const uint32_t t[4], uint32_t n)
+{
+    const uint32_t sel = n & 0x07070707u;
+    const uint32_t a = __builtin_amdgcn_perm(t[1], t[0], sel);  // entries 0..7
+    const uint32_t b = __builtin_amdgcn_perm(t[3], t[2], sel);  // entries 8..15
+    const uint32_t b3 = n & 0x08080808u;
+    const uint32_t m = (b3 << 5) - (b3 >> 3);                   // 0xFF where n >= 8
+    return (a & ~m) | (b & m);
+}
+
+__device__ __forceinline__ uint32_t gf_mulc(const NibTable& t, uint32_t x)
+{
+    return lut16(t.lo, x & 0x0f0f0f0fu) ^ lut16(t.hi, (x >> 4) & 0x0f0f0f0fu);
+}
+__device__ __forceinline__ u32x4 gf_mulc(const NibTable& t, u32x4 x)
+{
+    u32x4 r;
+    r.x = gf_mulc(t, x.x);
+    r.y = gf_mulc(t, x.y);
+    r.z = gf_mulc(t, x.z);
+    r.w = gf_mulc(t, x.w);
+    return r;
+}
+
+}  // namespace draid

@@ -1,0 +1,566 @@
+// ec_kernels.hip -- RAID5 XOR / RAID6 P+Q encode and reconstruct kernels for
+// MI355X (gfx950, CDNA4).
+//
+// Hot path: the full-stripe parity of
+//   raid5_stripe_write_preread_complete  module/bdev/raid/raid5.c:743-777
+//   raid5_xor_stripe                     module/bdev/raid/raid5_simple.c:141-203
+//   pq_gen                               examples/bdev/gf_vect_mul/gf_vect_mul.c:101
+// and the degraded-read reconstruct of
+//   raid5_complete_reconstructed_stripe_request  raid5.c:544-594
+//   D+P / D+D recovery                            gf_vect_mul.c:242-347
+//
+// Shape: one workgroup (256 lanes = 4 waves) owns one chunk of one stripe:
+// CB = 256 * U * 16 bytes of every strip.  Each lane holds U 16-byte vectors
+// per strip; with k known at compile time every source load of the lane is
+// issued before the first XOR, so a wave keeps (k+1)*U KiB in flight.  HBM is
+// the roofline: encode moves (k+m)*S algorithmic bytes per stripe and does
+// ~2 VALU ops per byte read, far below the VALU ceiling.  Workgroups are
+// independent (no inter-workgroup communication, no atomics on the hot path).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ec_gf.hpp"
+#include "ec_launch.hpp"
+
+namespace draid {
+
+constexpr int kThreads = 256;
+// Largest strip a launch accepts: in-kernel offsets are 32-bit.
+constexpr uint64_t kMaxStripLen = 0x7fff0000ull;
+
+__constant__ GfTables c_gf = make_gf_tables();
+
+static int g_variant = 0;
+void set_variant(int v) { g_variant = v; }
+int get_variant() { return g_variant; }
+
+// ------------------------------------------------------------ pointers
+
+struct TablePtrs {
+    const uint8_t* const* tab;
+    uint32_t stride;
+    __device__ __forceinline__ const uint8_t* get(uint32_t s, int j) const
+    {
+        return tab[(size_t)s * stride + j];
+    }
+};
+
+struct ArgPtrs {
+    ArgPtrTable t;
+    __device__ __forceinline__ const uint8_t* get(uint32_t, int j) const { return t.p[j]; }
+};
+
+// ------------------------------------------------------------ memory words
+
+// Strip pointers come from a table of generic pointers; casting to the global
+// address space lets the compiler emit global_load/store with the uniform strip
+// base in SGPRs and a 32-bit per-lane offset (saddr + voffset form) instead of
+// flat instructions with 64-bit per-lane addresses.
+typedef const u32x4 __attribute__((address_space(1)))* gcv4;
+typedef u32x4 __attribute__((address_space(1)))* gv4;
+typedef const uint8_t __attribute__((address_space(1)))* gcb;
+typedef uint8_t __attribute__((address_space(1)))* gb;
+
+// W = u32x4: one 16-byte vector, index in vectors.  W = uint32_t: one byte
+// held in the low 8 bits, index in bytes (tails and unaligned strips).
+// Indices are 32-bit: strips are < 4 GiB (checked on the host).
+template <class W>
+struct Mem;
+
+template <>
+struct Mem<u32x4> {
+    template <bool NT>
+    static __device__ __forceinline__ u32x4 ld(const uint8_t* p, uint32_t i)
+    {
+        gcv4 q = (gcv4)(p + (i << 4));
+        if constexpr (NT)
+            return __builtin_nontemporal_load(q);
+        else
+            return *q;
+    }
+    template <bool NT>
+    static __device__ __forceinline__ void st(const uint8_t* p, uint32_t i, u32x4 v)
+    {
+        gv4 q = (gv4)(const_cast<uint8_t*>(p) + (i << 4));
+        if constexpr (NT)
+            __builtin_nontemporal_store(v, q);
+        else
+            *q = v;
+    }
+    static __device__ __forceinline__ bool any(u32x4 v) { return (v.x | v.y | v.z | v.w) != 0; }
+};
+
+template <>
+struct Mem<uint32_t> {
+    template <bool NT>
+    static __device__ __forceinline__ uint32_t ld(const uint8_t* p, uint32_t i)
+    {
+        return *((gcb)p + i);
+    }
+    template <bool NT>
+    static __device__ __forceinline__ void st(const uint8_t* p, uint32_t i, uint32_t v)
+    {
+        *((gb)const_cast<uint8_t*>(p) + i) = static_cast<uint8_t>(v);
+    }
+    static __device__ __forceinline__ bool any(uint32_t v) { return (v & 0xffu) != 0; }
+};
+
+// Calls f(j) for j = k-1 down to 0; fully unrolled when k is a template constant.
+template <int KT, class F>
+__device__ __forceinline__ void for_sources_desc(int k, F&& f)
+{
+    if constexpr (KT > 0) {
+#pragma unroll
+        for (int j = KT - 1; j >= 0; --j)
+            f(j);
+    } else {
+        for (int j = k - 1; j >= 0; --j)
+            f(j);
+    }
+}
+
+// ------------------------------------------------------------ encode core
+
+// Computes P (and Q for M == 2) over the U elements i0 + u*stride (< n) and
+// either stores them (CHECK == false) or compares them with the stored parity.
+// BOUNDED == false: the caller guarantees every element is in range (full
+// chunks), so no load or store is predicated.
+template <int KT, int M, int U, bool NT, bool CHECK, bool BOUNDED, class W, class Ptrs>
+__device__ __forceinline__ bool encode_elems(const Ptrs& pp, uint32_t s, int k, uint32_t i0,
+                                             uint32_t stride, uint32_t n)
+{
+    using MW = Mem<W>;
+    W p[U], q[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        ok[u] = !BOUNDED || i0 + u * stride < n;
+        p[u] = W(0);
+        q[u] = W(0);
+    }
+    for_sources_desc<KT>(k, [&](int j) {
+        const uint8_t* src = pp.get(s, j);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const W d = ok[u] ? MW::template ld<NT>(src, i0 + u * stride) : W(0);
+            p[u] ^= d;
+            if constexpr (M == 2)
+                q[u] = gf_mul2(q[u]) ^ d;
+        }
+    });
+    const uint8_t* dp = pp.get(s, k);
+    const uint8_t* dq = (M == 2) ? pp.get(s, k + 1) : nullptr;
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!ok[u])
+            continue;
+        const uint32_t i = i0 + u * stride;
+        if constexpr (CHECK) {
+            bad |= MW::any(MW::template ld<false>(dp, i) ^ p[u]);
+            if constexpr (M == 2)
+                bad |= MW::any(MW::template ld<false>(dq, i) ^ q[u]);
+        } else {
+            MW::template st<NT>(dp, i, p[u]);
+            if constexpr (M == 2)
+                MW::template st<NT>(dq, i, q[u]);
+        }
+    }
+    return bad;
+}
+
+template <int KT, int M, class Ptrs>
+__device__ __forceinline__ bool stripe_aligned(const Ptrs& pp, uint32_t s, int k)
+{
+    uintptr_t acc = 0;
+    if constexpr (KT > 0) {
+#pragma unroll
+        for (int j = 0; j < KT + M; ++j)
+            acc |= reinterpret_cast<uintptr_t>(pp.get(s, j));
+    } else {
+        for (int j = 0; j < k + M; ++j)
+            acc |= reinterpret_cast<uintptr_t>(pp.get(s, j));
+    }
+    return (acc & 15u) == 0;
+}
+
+template <int KT, int M, int U, bool NT, bool CHECK, class Ptrs>
+__global__ __launch_bounds__(kThreads) void k_encode(Ptrs pp, uint32_t k_rt, uint32_t len,
+                                                     uint32_t cps, uint32_t* flag)
+{
+    const uint32_t s = blockIdx.x / cps;
+    const uint32_t c = blockIdx.x - s * cps;
+    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
+    constexpr uint32_t EPB = static_cast<uint32_t>(kThreads) * U;  // vectors per block
+    const uint32_t nvec = len >> 4;
+    bool bad = false;
+    if (stripe_aligned<KT, M>(pp, s, k)) {
+        const uint32_t i0 = c * EPB + threadIdx.x;
+        if ((c + 1) * EPB <= nvec)
+            bad = encode_elems<KT, M, U, NT, CHECK, false, u32x4>(pp, s, k, i0, kThreads, nvec);
+        else
+            bad = encode_elems<KT, M, U, NT, CHECK, true, u32x4>(pp, s, k, i0, kThreads, nvec);
+        const uint32_t tail = len & 15u;
+        if (tail && c == cps - 1 && threadIdx.x < tail)
+            bad |= encode_elems<0, M, 1, false, CHECK, true, uint32_t>(
+                pp, s, k, nvec * 16 + threadIdx.x, kThreads, len);
+    } else {
+        const uint32_t b1 = min(len, (c + 1) * EPB * 16);
+        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += kThreads)
+            bad |= encode_elems<0, M, 1, false, CHECK, true, uint32_t>(pp, s, k, b, kThreads, b1);
+    }
+    if constexpr (CHECK) {
+        if (bad)
+            atomicOr(flag, 1u);
+    }
+}
+
+// ------------------------------------------------------------ reconstruct
+
+// Per-stripe recovery plan; every value is uniform across the workgroup.
+struct RecPlan {
+    int x, y;          // lost data strips (x < y), -1 = none
+    int nd;            // number of lost data strips
+    bool lostP, lostQ; // parity strips to regenerate
+    bool needq;        // the Q syndrome over the survivors is needed
+    bool skip;         // unrecoverable / nothing to do
+    NibTable t1, t2;   // constant multipliers (see build_plan)
+};
+
+// Decodes the failure pair and derives the GF constants from the exp/log
+// tables staged in LDS (gf_vect_mul.c:296-326 for the D+D constants).
+template <int M>
+__device__ __forceinline__ RecPlan build_plan(int k, uint32_t f0, uint32_t f1, const uint8_t* s_exp,
+                                              const uint8_t* s_log)
+{
+    RecPlan pl;
+    pl.x = -1;
+    pl.y = -1;
+    pl.nd = 0;
+    pl.lostP = false;
+    pl.lostQ = false;
+    const uint32_t f[2] = {f0, f1};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int j = static_cast<int>(f[t]);
+        if (f[t] == 0xffu || j >= k + M)
+            continue;
+        if (j < k) {
+            if (pl.nd == 1 && pl.x == j)
+                continue;
+            if (pl.nd == 0)
+                pl.x = j;
+            else
+                pl.y = j;
+            ++pl.nd;
+        } else if (j == k) {
+            pl.lostP = true;
+        } else {
+            pl.lostQ = true;
+        }
+    }
+    if (pl.nd == 2 && pl.x > pl.y) {
+        const int t = pl.x;
+        pl.x = pl.y;
+        pl.y = t;
+    }
+    const int nf = pl.nd + (pl.lostP ? 1 : 0) + (pl.lostQ ? 1 : 0);
+    pl.skip = (nf == 0) || (nf > M);
+    pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
+    uint32_t c1 = 0, c2 = 0;
+    if (pl.nd == 1 && !pl.lostP && pl.lostQ) {
+        c1 = s_exp[pl.x];                       // Q = Qs ^ 2^x D_x
+    } else if (pl.nd == 1 && pl.lostP) {
+        c1 = s_exp[255 - pl.x];                 // D_x = 2^-x (Q ^ Qs)
+    } else if (pl.nd == 2) {
+        const uint32_t gyx = s_exp[pl.y - pl.x];
+        const uint32_t den = s_exp[255 - s_log[gyx ^ 1u]];           // 1 / (2^(y-x) ^ 1)
+        c1 = s_exp[s_log[gyx] + s_log[den]];                         // A = 2^(y-x) / (...)
+        c2 = s_exp[(255 - pl.x) + s_log[den]];                       // B = 2^-x / (...)
+    }
+    pl.t1 = make_nib_table(c1);
+    pl.t2 = make_nib_table(c2);
+    return pl;
+}
+
+template <int KT, int M, int U, bool NT, bool BOUNDED, class W, class Ptrs>
+__device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k, const RecPlan& pl,
+                                              uint32_t i0, uint32_t stride, uint32_t n)
+{
+    using MW = Mem<W>;
+    const uint8_t* pP = pp.get(s, k);
+    const uint8_t* pQ = (M == 2) ? pp.get(s, k + 1) : pP;
+    // A strip that is lost (or not needed) is loaded from `sub` instead -- an
+    // address this lane loads anyway, so the duplicate is a cache hit -- and
+    // masked to zero.  That keeps every load unconditional and batched.
+    const uint8_t* sub = pl.lostP ? pQ : pP;
+    const bool useQ = pl.needq && !pl.lostQ;
+    W ps[U], qs[U], pv[U], qv[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        ok[u] = !BOUNDED || i0 + u * stride < n;
+        ps[u] = W(0);
+        qs[u] = W(0);
+        pv[u] = ok[u] ? MW::template ld<NT>(pl.lostP ? sub : pP, i0 + u * stride) : W(0);
+        qv[u] = ok[u] ? MW::template ld<NT>(useQ ? pQ : sub, i0 + u * stride) : W(0);
+    }
+    for_sources_desc<KT>(k, [&](int j) {
+        const bool dead = (j == pl.x) || (j == pl.y);
+        const uint8_t* src = dead ? sub : pp.get(s, j);
+        const uint32_t keep = dead ? 0u : 0xffffffffu;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const W d = (ok[u] ? MW::template ld<NT>(src, i0 + u * stride) : W(0)) & keep;
+            ps[u] ^= d;
+            if constexpr (M == 2)
+                qs[u] = gf_mul2(qs[u]) ^ d;
+        }
+    });
+    const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
+    const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!ok[u])
+            continue;
+        const uint32_t i = i0 + u * stride;
+        if (pl.nd == 0) {
+            if (pl.lostP)
+                MW::template st<NT>(pP, i, ps[u]);
+            if (M == 2 && pl.lostQ)
+                MW::template st<NT>(pQ, i, qs[u]);
+        } else if (pl.nd == 1) {
+            if (!pl.lostP) {
+                const W dx = pv[u] ^ ps[u];
+                MW::template st<NT>(pX, i, dx);
+                if (M == 2 && pl.lostQ)
+                    MW::template st<NT>(pQ, i, qs[u] ^ gf_mulc(pl.t1, dx));
+            } else {
+                const W dx = gf_mulc(pl.t1, qv[u] ^ qs[u]);
+                MW::template st<NT>(pX, i, dx);
+                MW::template st<NT>(pP, i, ps[u] ^ dx);
+            }
+        } else {
+            const W pxy = pv[u] ^ ps[u];
+            const W qxy = qv[u] ^ qs[u];
+            const W dx = gf_mulc(pl.t1, pxy) ^ gf_mulc(pl.t2, qxy);
+            MW::template st<NT>(pX, i, dx);
+            MW::template st<NT>(pY, i, pxy ^ dx);
+        }
+    }
+}
+
+template <int KT, int M, int U, bool NT, class Ptrs>
+__global__ __launch_bounds__(kThreads) void k_reconstruct(Ptrs pp, uint32_t k_rt, uint32_t len,
+                                                          uint32_t cps, const uint8_t* fail,
+                                                          uint32_t f01)
+{
+    // LDS-staged exp/log tables (768 B) for the per-stripe constants.
+    __shared__ uint32_t s_tab[(512 + 256) / 4];
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(&c_gf);
+    for (int t = threadIdx.x; t < (512 + 256) / 4; t += kThreads)
+        s_tab[t] = g[t];
+    __syncthreads();
+    const uint8_t* s_exp = reinterpret_cast<const uint8_t*>(s_tab);
+    const uint8_t* s_log = s_exp + 512;
+
+    const uint32_t s = blockIdx.x / cps;
+    const uint32_t c = blockIdx.x - s * cps;
+    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
+    uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
+    if (fail) {
+        f0 = fail[2 * (size_t)s];
+        f1 = fail[2 * (size_t)s + 1];
+    }
+    const RecPlan pl = build_plan<M>(k, f0, f1, s_exp, s_log);
+    if (pl.skip)
+        return;
+    constexpr uint32_t EPB = static_cast<uint32_t>(kThreads) * U;
+    const uint32_t nvec = len >> 4;
+    if (stripe_aligned<KT, M>(pp, s, k)) {
+        const uint32_t i0 = c * EPB + threadIdx.x;
+        if ((c + 1) * EPB <= nvec)
+            recover_elems<KT, M, U, NT, false, u32x4>(pp, s, k, pl, i0, kThreads, nvec);
+        else
+            recover_elems<KT, M, U, NT, true, u32x4>(pp, s, k, pl, i0, kThreads, nvec);
+        const uint32_t tail = len & 15u;
+        if (tail && c == cps - 1 && threadIdx.x < tail)
+            recover_elems<0, M, 1, false, true, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
+                                                          kThreads, len);
+    } else {
+        const uint32_t b1 = min(len, (c + 1) * EPB * 16);
+        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += kThreads)
+            recover_elems<0, M, 1, false, true, uint32_t>(pp, s, k, pl, b, kThreads, b1);
+    }
+}
+
+// ------------------------------------------------------------ gf_vect_mul
+
+__global__ __launch_bounds__(kThreads) void k_gf_vect_mul(const uint8_t* src, uint8_t* dst,
+                                                          uint32_t len, NibTable t)
+{
+    const uint32_t tid = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t nth = gridDim.x * kThreads;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
+        const uint32_t nvec = len >> 4;
+        for (uint32_t i = tid; i < nvec; i += nth)
+            Mem<u32x4>::st<false>(dst, i, gf_mulc(t, Mem<u32x4>::ld<false>(src, i)));
+        for (uint32_t b = nvec * 16 + tid; b < len; b += nth)
+            Mem<uint32_t>::st<false>(dst, b, gf_mulc(t, Mem<uint32_t>::ld<false>(src, b)));
+    } else {
+        for (uint32_t b = tid; b < len; b += nth)
+            Mem<uint32_t>::st<false>(dst, b, gf_mulc(t, Mem<uint32_t>::ld<false>(src, b)));
+    }
+}
+
+// ------------------------------------------------------------ launchers
+
+// Vectors per lane per strip: fewer sources -> more vectors, so a lane always
+// has roughly 8-16 loads of 16 B in flight.
+constexpr int unroll_for(int k) { return k <= 4 ? 4 : (k <= 8 ? 2 : 1); }
+
+static inline uint32_t chunks_per_stripe(uint64_t len, int U)
+{
+    const uint64_t cb = static_cast<uint64_t>(kThreads) * U * 16;
+    const uint64_t c = (len + cb - 1) / cb;
+    return static_cast<uint32_t>(c == 0 ? 1 : c);
+}
+
+template <int KT, int M, bool NT, bool CHECK, class Ptrs>
+static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
+                            uint32_t* flag, hipStream_t st)
+{
+    constexpr int U = KT > 0 ? unroll_for(KT) : 2;
+    const uint32_t cps = chunks_per_stripe(len, U);
+    const uint64_t blocks = static_cast<uint64_t>(cps) * nstripes;
+    if (blocks == 0)
+        return hipSuccess;
+    if (blocks > 0x7fffffffull || len > kMaxStripLen)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_encode<KT, M, U, NT, CHECK, Ptrs>), dim3(static_cast<uint32_t>(blocks)),
+                       dim3(kThreads), 0, st, pp, k, static_cast<uint32_t>(len), cps, flag);
+    return hipGetLastError();
+}
+
+template <int KT, int M, bool NT, class Ptrs>
+static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
+                                 const uint8_t* fail, uint32_t f01, hipStream_t st)
+{
+    constexpr int U = KT > 0 ? unroll_for(KT) : 2;
+    const uint32_t cps = chunks_per_stripe(len, U);
+    const uint64_t blocks = static_cast<uint64_t>(cps) * nstripes;
+    if (blocks == 0)
+        return hipSuccess;
+    if (blocks > 0x7fffffffull || len > kMaxStripLen)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_reconstruct<KT, M, U, NT, Ptrs>), dim3(static_cast<uint32_t>(blocks)),
+                       dim3(kThreads), 0, st, pp, k, static_cast<uint32_t>(len), cps, fail, f01);
+    return hipGetLastError();
+}
+
+// k values with a fully unrolled instantiation; others use the runtime-k loop.
+#define DRAID_FOR_EACH_K(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(12) X(14) X(16)
+
+template <int M, bool NT, class Ptrs>
+static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
+                                  hipStream_t st)
+{
+    switch (k) {
+#define DRAID_CASE(K) \
+    case K:           \
+        return go_encode<K, M, NT, false>(pp, k, len, nstripes, nullptr, st);
+        DRAID_FOR_EACH_K(DRAID_CASE)
+#undef DRAID_CASE
+    default:
+        return go_encode<0, M, NT, false>(pp, k, len, nstripes, nullptr, st);
+    }
+}
+
+template <int M, bool NT, class Ptrs>
+static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
+                                       uint32_t nstripes, const uint8_t* fail, uint32_t f01,
+                                       hipStream_t st)
+{
+    switch (k) {
+#define DRAID_CASE(K) \
+    case K:           \
+        return go_reconstruct<K, M, NT>(pp, k, len, nstripes, fail, f01, st);
+        DRAID_FOR_EACH_K(DRAID_CASE)
+#undef DRAID_CASE
+    default:
+        return go_reconstruct<0, M, NT>(pp, k, len, nstripes, fail, f01, st);
+    }
+}
+
+hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                         const uint8_t* const* table, const ArgPtrTable* args, hipStream_t st)
+{
+    if (table) {
+        const TablePtrs pp{table, k + m};
+        const bool nt = g_variant != 1;
+        if (m == 1)
+            return nt ? dispatch_encode<1, true>(pp, k, len, nstripes, st)
+                      : dispatch_encode<1, false>(pp, k, len, nstripes, st);
+        return nt ? dispatch_encode<2, true>(pp, k, len, nstripes, st)
+                  : dispatch_encode<2, false>(pp, k, len, nstripes, st);
+    }
+    const ArgPtrs pp{*args};
+    if (m == 1)
+        return dispatch_encode<1, true>(pp, k, len, 1, st);
+    return dispatch_encode<2, true>(pp, k, len, 1, st);
+}
+
+hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                              const uint8_t* const* table, const ArgPtrTable* args,
+                              const uint8_t* fail_dev, uint8_t f0, uint8_t f1, hipStream_t st)
+{
+    const uint32_t f01 = static_cast<uint32_t>(f0) | (static_cast<uint32_t>(f1) << 8);
+    if (table) {
+        const TablePtrs pp{table, k + m};
+        if (m == 1)
+            return dispatch_reconstruct<1, true>(pp, k, len, nstripes, fail_dev, f01, st);
+        return dispatch_reconstruct<2, true>(pp, k, len, nstripes, fail_dev, f01, st);
+    }
+    const ArgPtrs pp{*args};
+    if (m == 1)
+        return dispatch_reconstruct<1, true>(pp, k, len, 1, fail_dev, f01, st);
+    return dispatch_reconstruct<2, true>(pp, k, len, 1, fail_dev, f01, st);
+}
+
+hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* const* table,
+                        const ArgPtrTable* args, uint32_t* flag, hipStream_t st)
+{
+    if (table) {
+        const TablePtrs pp{table, k + m};
+        return m == 1 ? go_encode<0, 1, false, true>(pp, k, len, 1, flag, st)
+                      : go_encode<0, 2, false, true>(pp, k, len, 1, flag, st);
+    }
+    const ArgPtrs pp{*args};
+    return m == 1 ? go_encode<0, 1, false, true>(pp, k, len, 1, flag, st)
+                  : go_encode<0, 2, false, true>(pp, k, len, 1, flag, st);
+}
+
+hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,
+                              uint8_t* dst, hipStream_t st)
+{
+    if (len == 0)
+        return hipSuccess;
+    if (len > kMaxStripLen)
+        return hipErrorInvalidValue;
+    NibTable t;
+    for (int w = 0; w < 4; ++w) {
+        t.lo[w] = tbl[4 * w] | (tbl[4 * w + 1] << 8) | (tbl[4 * w + 2] << 16) |
+                  (static_cast<uint32_t>(tbl[4 * w + 3]) << 24);
+        t.hi[w] = tbl[16 + 4 * w] | (tbl[16 + 4 * w + 1] << 8) | (tbl[16 + 4 * w + 2] << 16) |
+                  (static_cast<uint32_t>(tbl[16 + 4 * w + 3]) << 24);
+    }
+    const uint64_t vec = (len + 15) / 16;
+    uint64_t blocks = (vec + kThreads - 1) / kThreads;
+    if (blocks > 4096)
+        blocks = 4096;
+    hipLaunchKernelGGL(k_gf_vect_mul, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, st,
+                       src, dst, static_cast<uint32_t>(len), t);
+    return hipGetLastError();
+}
+
+}  // namespace draid

@@ -1,0 +1,45 @@
+// ec_launch.hpp -- internal launcher interface between the C ABI (ec_api.cpp)
+// and the HIP kernels (ec_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace draid {
+
+// Pointers for the synchronous isa-l-shaped calls travel in the kernel
+// arguments (one stripe); above this many vectors they go through a device table.
+constexpr int kMaxArgPtrs = 34;
+
+struct ArgPtrTable {
+    const uint8_t* p[kMaxArgPtrs];
+};
+
+// Encode: m = 1 (XOR parity) or 2 (P+Q).
+//   table != nullptr : device table [nstripes][k+m]
+//   table == nullptr : *args holds the k+m pointers of one stripe (nstripes == 1)
+hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                         const uint8_t* const* table, const ArgPtrTable* args,
+                         hipStream_t stream);
+
+// Reconstruct.  fail_dev: device [nstripes][2] (0xFF = none); when null,
+// (f0, f1) apply to every stripe.
+hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                              const uint8_t* const* table, const ArgPtrTable* args,
+                              const uint8_t* fail_dev, uint8_t f0, uint8_t f1,
+                              hipStream_t stream);
+
+// Check: sets *flag_dev to non-zero if any stored parity differs.
+hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len,
+                        const uint8_t* const* table, const ArgPtrTable* args,
+                        uint32_t* flag_dev, hipStream_t stream);
+
+// dest = c * src (c given by its isa-l 32-byte nibble table).
+hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,
+                              uint8_t* dst, hipStream_t stream);
+
+// Variant selector for A/B experiments inside one process (0 = default).
+void set_variant(int v);
+int get_variant();
+
+}  // namespace draid

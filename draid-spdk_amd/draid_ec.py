@@ -1,0 +1,187 @@
+"""ctypes binding of libdraid_ec.so (the C ABI in include/draid_ec.h).
+
+Plumbing for tests and bench.py: it passes raw device pointers (from torch
+tensors or draid_ec_device_alloc) straight to the C ABI -- no torch types cross
+the boundary.  There is no fallback: if the shared library is missing or the GPU
+is unusable every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdraid_ec.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "draid_ec.h")
+
+FAIL_NONE = 0xFF
+
+# Every symbol include/draid_ec.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "draid_xor_gen", "draid_pq_gen", "draid_xor_check", "draid_pq_check",
+    "draid_gf_mul", "draid_gf_inv", "draid_gf_vect_mul_init", "draid_gf_vect_mul",
+    "draid_recover", "draid_ec_encode", "draid_ec_reconstruct",
+    "draid_ec_abi_version", "draid_ec_last_error", "draid_ec_set_device",
+    "draid_ec_device_count", "draid_ec_stream_create", "draid_ec_stream_destroy",
+    "draid_ec_stream_query", "draid_ec_stream_synchronize", "draid_ec_device_alloc",
+    "draid_ec_device_free", "draid_ec_host_register", "draid_ec_host_unregister",
+    "draid_ec_memcpy_async",
+)
+
+
+class StripeBatch(C.Structure):
+    _fields_ = [
+        ("k", C.c_uint32),
+        ("m", C.c_uint32),
+        ("strip_len", C.c_uint64),
+        ("nstripes", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("strips", C.c_void_p),
+    ]
+
+
+class DraidError(RuntimeError):
+    pass
+
+
+def build(force: bool = False) -> str:
+    """Compile libdraid_ec.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", HERE, "libdraid_ec.so"])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DraidError(f"{LIB_PATH} is missing: run `make -C {HERE}` (no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        i32, vp, u8 = C.c_int, C.c_void_p, C.c_ubyte
+        for f in ("draid_xor_gen", "draid_pq_gen", "draid_xor_check", "draid_pq_check"):
+            getattr(L, f).argtypes = [i32, i32, C.POINTER(vp)]
+            getattr(L, f).restype = i32
+        L.draid_gf_mul.argtypes = [u8, u8]
+        L.draid_gf_mul.restype = u8
+        L.draid_gf_inv.argtypes = [u8]
+        L.draid_gf_inv.restype = u8
+        L.draid_gf_vect_mul_init.argtypes = [u8, vp]
+        L.draid_gf_vect_mul.argtypes = [i32, vp, vp, vp]
+        L.draid_recover.argtypes = [i32, i32, i32, C.POINTER(vp), i32, C.POINTER(i32)]
+        L.draid_ec_encode.argtypes = [C.POINTER(StripeBatch), vp]
+        L.draid_ec_reconstruct.argtypes = [C.POINTER(StripeBatch), vp, vp]
+        L.draid_ec_last_error.restype = C.c_char_p
+        L.draid_ec_set_device.argtypes = [i32]
+        L.draid_ec_device_count.argtypes = [C.POINTER(i32)]
+        L.draid_ec_stream_create.argtypes = [C.POINTER(vp)]
+        for f in ("draid_ec_stream_destroy", "draid_ec_stream_query",
+                  "draid_ec_stream_synchronize", "draid_ec_device_free",
+                  "draid_ec_host_unregister"):
+            getattr(L, f).argtypes = [vp]
+        L.draid_ec_device_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
+        L.draid_ec_host_register.argtypes = [vp, C.c_size_t]
+        L.draid_ec_memcpy_async.argtypes = [vp, vp, C.c_size_t, i32, vp]
+        L.draid_ec_set_variant.argtypes = [i32]
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().draid_ec_last_error().decode()
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise DraidError(f"{what} failed ({rc}): {last_error()}")
+    return rc
+
+
+def _ptr(x) -> int:
+    return x if isinstance(x, int) else x.data_ptr()
+
+
+def _array(ptrs) -> C.Array:
+    return (C.c_void_p * len(ptrs))(*[_ptr(p) for p in ptrs])
+
+
+# ---- isa-l-shaped synchronous calls (device pointers) ----
+
+def xor_gen(ptrs, length: int) -> int:
+    return _check(lib().draid_xor_gen(len(ptrs), length, _array(ptrs)), "xor_gen")
+
+
+def pq_gen(ptrs, length: int) -> int:
+    return _check(lib().draid_pq_gen(len(ptrs), length, _array(ptrs)), "pq_gen")
+
+
+def xor_check(ptrs, length: int) -> int:
+    return _check(lib().draid_xor_check(len(ptrs), length, _array(ptrs)), "xor_check")
+
+
+def pq_check(ptrs, length: int) -> int:
+    return _check(lib().draid_pq_check(len(ptrs), length, _array(ptrs)), "pq_check")
+
+
+def gf_mul(a: int, b: int) -> int:
+    return lib().draid_gf_mul(a, b)
+
+
+def gf_inv(a: int) -> int:
+    return lib().draid_gf_inv(a)
+
+
+def gf_vect_mul_init(c: int) -> bytes:
+    buf = (C.c_ubyte * 32)()
+    lib().draid_gf_vect_mul_init(c, buf)
+    return bytes(buf)
+
+
+def gf_vect_mul(length: int, tbl: bytes, src, dst) -> int:
+    t = (C.c_ubyte * 32)(*tbl)
+    return _check(lib().draid_gf_vect_mul(length, t, _ptr(src), _ptr(dst)), "gf_vect_mul")
+
+
+def recover(k: int, m: int, length: int, ptrs, fail) -> int:
+    f = (C.c_int * max(1, len(fail)))(*fail)
+    return _check(lib().draid_recover(k, m, length, _array(ptrs), len(fail), f), "recover")
+
+
+# ---- batched asynchronous API ----
+
+def make_batch(k: int, m: int, strip_len: int, nstripes: int, table_ptr) -> StripeBatch:
+    return StripeBatch(k, m, strip_len, nstripes, 0, _ptr(table_ptr))
+
+
+def encode(batch: StripeBatch, stream: int) -> int:
+    return _check(lib().draid_ec_encode(C.byref(batch), stream), "ec_encode")
+
+
+def reconstruct(batch: StripeBatch, fail_ptr, stream: int) -> int:
+    return _check(lib().draid_ec_reconstruct(C.byref(batch), _ptr(fail_ptr), stream),
+                  "ec_reconstruct")
+
+
+def stream_create() -> int:
+    s = C.c_void_p()
+    _check(lib().draid_ec_stream_create(C.byref(s)), "stream_create")
+    return s.value
+
+
+def stream_destroy(stream: int) -> None:
+    _check(lib().draid_ec_stream_destroy(stream), "stream_destroy")
+
+
+def stream_query(stream: int) -> int:
+    return _check(lib().draid_ec_stream_query(stream), "stream_query")
+
+
+def stream_synchronize(stream: int) -> None:
+    _check(lib().draid_ec_stream_synchronize(stream), "stream_synchronize")
+
+
+def set_variant(v: int) -> None:
+    lib().draid_ec_set_variant(v)

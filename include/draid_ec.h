@@ -1,0 +1,142 @@
+/*
+ * draid_ec.h -- C ABI of the MI355X erasure-coding engine (libdraid_ec.so).
+ *
+ * Drop-in boundary for the parity hot path of kyleshu/draid-spdk's RAID
+ * bdev modules (module/bdev/raid/).  Two nested surfaces, as SURVEY.md §8b
+ * describes:
+ *
+ *  1. The isa-l v2.30 arithmetic ABI the raid modules call (raid.h /
+ *     gf_vect_mul.h), re-implemented as HIP kernels on gfx950.  Same argument
+ *     meaning, same array order, same 0 / non-zero return convention.  Every
+ *     buffer pointer must be device-accessible (hipMalloc'd HBM, or host memory
+ *     registered with draid_ec_host_register()).  Calls are synchronous, like
+ *     isa-l's: they run on the calling thread's per-thread stream and return
+ *     once the result is in memory.
+ *
+ *  2. A batched, asynchronous stripe API for the GPU path proper: many
+ *     independent stripes per launch through a device-resident pointer table,
+ *     enqueued on a caller-owned stream so an SPDK reactor never blocks (the
+ *     raid module keeps one stream per io_channel and completes requests from
+ *     a poller on draid_ec_stream_query()).
+ *
+ * No torch or HIP types appear in these signatures: streams are `void *`
+ * (a hipStream_t underneath), memory is plain pointers and sizes.
+ *
+ * Return convention: 0 = success; 1 = the arguments are rejected with
+ * isa-l's semantics (nothing written); negative = HIP runtime failure
+ * (draid_ec_last_error() has the message).
+ */
+#ifndef DRAID_EC_H
+#define DRAID_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRAID_EC_ABI_VERSION 1
+#define DRAID_EC_FAIL_NONE 0xFFu /* unused slot of a per-stripe failure pair */
+
+/* ------------------------------------------------------------------------
+ * 1. isa-l-shaped synchronous entry points
+ * ---------------------------------------------------------------------- */
+
+/* XOR parity: array[vects-1] = XOR of array[0 .. vects-2], len bytes each.
+ * Replaces isa-l xor_gen() (isa-l/include/raid.h, v2.30) as called by
+ *   raid5_xor_buf        module/bdev/raid/raid5.c:188-201   (vects = 3, in place)
+ *   raid5_xor_gen        module/bdev/raid/raid5_simple.c:131-135,176 (vects = k+1)
+ *   xor_buf              examples/bdev/gf_vect_mul/gf_vect_mul.c:40-49
+ * vects < 3 or len < 0 -> 1.  The destination may alias a source. */
+int draid_xor_gen(int vects, int len, void **array);
+
+/* P+Q parity: k = vects-2 sources; array[k] = P = XOR_j D_j,
+ * array[k+1] = Q = XOR_j 2^j D_j over GF(2^8)/0x11D.
+ * Replaces isa-l pq_gen() as called at gf_vect_mul.c:101,152,199,253,294.
+ * vects < 4, len < 0 or len % 32 != 0 -> 1 (isa-l's SIMD contract). */
+int draid_pq_gen(int vects, int len, void **array);
+
+/* 0 iff XOR over all vects pointers is zero (isa-l xor_check()). */
+int draid_xor_check(int vects, int len, void **array);
+
+/* 0 iff array[k], array[k+1] hold the P, Q of array[0..k-1]
+ * (isa-l pq_check(); used at gf_vect_mul.c:178-179). */
+int draid_pq_check(int vects, int len, void **array);
+
+/* GF(2^8) scalar helpers (host-side; isa-l erasure_code.h gf_mul / gf_inv,
+ * gf_vect_mul.h gf_vect_mul_init -- gf_vect_mul.c:60-66,313-322). */
+unsigned char draid_gf_mul(unsigned char a, unsigned char b);
+unsigned char draid_gf_inv(unsigned char a);
+void draid_gf_vect_mul_init(unsigned char c, unsigned char *tbl /* [32] */);
+
+/* dest = c * src over len bytes, with tbl from draid_gf_vect_mul_init(c).
+ * Replaces isa-l gf_vect_mul() (gf_vect_mul.c:108,158,221,256,267,310-326).
+ * len < 0 or len % 32 != 0 -> 1. src and dest may alias. */
+int draid_gf_vect_mul(int len, unsigned char *tbl, void *src, void *dest);
+
+/* Composite recovery of one stripe (the compositions of
+ * raid5.c:544-594 and gf_vect_mul.c:242-347 as one kernel):
+ * array = k data pointers, then P (array[k]) and, for m == 2, Q (array[k+1]).
+ * The nfail (<= m) strips listed in fail[] are regenerated in place.
+ * Invalid or unrecoverable failure sets -> 1. */
+int draid_recover(int k, int m, int len, void **array, int nfail, const int *fail);
+
+/* ------------------------------------------------------------------------
+ * 2. Batched asynchronous stripe API
+ * ---------------------------------------------------------------------- */
+
+typedef struct draid_ec_stripe_batch {
+    uint32_t k;            /* data strips per stripe, 1 .. 255                */
+    uint32_t m;            /* parity strips: 1 = RAID5 (P), 2 = RAID6 (P, Q)  */
+    uint64_t strip_len;    /* bytes per strip (same for every stripe)         */
+    uint32_t nstripes;     /* stripes in this batch                           */
+    uint32_t flags;        /* reserved, must be 0                             */
+    /* DEVICE-resident table of nstripes * (k + m) device pointers, stripe-major:
+     * strips[s*(k+m) + j] is data strip j (isa-l array order) for j < k,
+     * P for j == k, Q for j == k+1.  16-byte aligned strips run the vector
+     * path; any alignment is correct. */
+    void *const *strips;
+} draid_ec_stripe_batch;
+
+/* Full-stripe encode of every stripe in the batch (P for m == 1, P and Q for
+ * m == 2).  Enqueued on `stream`; returns without waiting. */
+int draid_ec_encode(const draid_ec_stripe_batch *batch, void *stream);
+
+/* Degraded-read / rebuild reconstruct.  `fail` is a DEVICE array of
+ * nstripes * 2 bytes: the (up to two) failed strip indices of each stripe
+ * (0..k-1 data, k = P, k+1 = Q; DRAID_EC_FAIL_NONE = unused).  The listed
+ * strips are regenerated into their table pointers.  Entries >= k+m are
+ * ignored; a stripe with more failures than m is left untouched. */
+int draid_ec_reconstruct(const draid_ec_stripe_batch *batch, const uint8_t *fail,
+                         void *stream);
+
+/* ------------------------------------------------------------------------
+ * 3. Runtime helpers (device, streams, memory)
+ * ---------------------------------------------------------------------- */
+
+int draid_ec_abi_version(void);
+const char *draid_ec_last_error(void);
+int draid_ec_set_device(int device);
+int draid_ec_device_count(int *count);
+
+int draid_ec_stream_create(void **stream);
+int draid_ec_stream_destroy(void *stream);
+/* 0 = all enqueued work done, 1 = still running, < 0 = error.  Non-blocking:
+ * the SPDK poller of a raid io_channel calls this. */
+int draid_ec_stream_query(void *stream);
+int draid_ec_stream_synchronize(void *stream);
+
+int draid_ec_device_alloc(void **ptr, size_t bytes);
+int draid_ec_device_free(void *ptr);
+/* Pin + map an existing host range (e.g. spdk_dma_malloc hugepages,
+ * raid5.c:1340-1342) so kernels and DMA can reach it. */
+int draid_ec_host_register(void *ptr, size_t bytes);
+int draid_ec_host_unregister(void *ptr);
+/* kind: 0 host->device, 1 device->host, 2 device->device. */
+int draid_ec_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRAID_EC_H */

@@ -1,0 +1,337 @@
+"""GPU parity tests: the HIP path through the C ABI, bit-exact against the CPU
+oracle and the golden fixtures.  Sizes: the oracle-checked cases finish in
+seconds; the BASELINE-sized cases check size-independent properties
+(encode -> erase -> reconstruct round trips, sampled stripes vs the oracle).
+"""
+import itertools
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy()
+
+
+class Batch:
+    """nstripes stripes of k+m strips laid out stripe-major in one device buffer,
+    with an optional gap between strips, plus the device pointer table."""
+
+    def __init__(self, k, m, L, B, gap=0, offset=0, data=None, seed=0):
+        self.k, self.m, self.L, self.B = k, m, L, B
+        self.strip_stride = L + gap
+        self.stripe_stride = (k + m) * self.strip_stride
+        total = B * self.stripe_stride + offset + 64
+        self.buf = torch.zeros(total, dtype=torch.uint8, device=DEV)
+        self.offset = offset
+        if data is None:
+            g = torch.Generator(device=DEV)
+            g.manual_seed(seed)
+            view = self.view()
+            view[:, :k, :L] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=DEV,
+                                            generator=g)
+        else:
+            self.view()[:, :, :L] = dev(data)
+        base = self.buf.data_ptr() + offset
+        ptrs = [base + s * self.stripe_stride + j * self.strip_stride
+                for s in range(B) for j in range(k + m)]
+        self.table = torch.tensor(ptrs, dtype=torch.int64, device=DEV)
+
+    def view(self):
+        return self.buf[self.offset:self.offset + self.B * self.stripe_stride].view(
+            self.B, self.k + self.m, self.strip_stride)
+
+    def strips(self):
+        return self.view()[:, :, :self.L]
+
+    def batch(self, ec):
+        return ec.make_batch(self.k, self.m, self.L, self.B, self.table)
+
+
+def oracle_encode(stripes: np.ndarray, k: int, m: int) -> np.ndarray:
+    """stripes: [B, k+m, L] -> copy with parity from the C oracle."""
+    out = np.ascontiguousarray(stripes.copy())
+    B, n, L = out.shape
+    flat = out.reshape(-1)
+    assert oracle.encode_strided(flat, k, m, L, B, L, n * L) == 0
+    return out
+
+
+def sync():
+    torch.cuda.synchronize()
+
+
+# ------------------------------------------------------------ isa-l shaped
+
+def test_pq_gen_gf_vect_mul_example(ec, golden):
+    """gf_vect_mul.c inputs (glibc srand(0x1234)) -> P||Q fixtures, via draid_pq_gen."""
+    K, L = 14, 4096
+    gm = golden["gf_vect_mul_example"]
+    oracle.srand(0x1234)
+    for name in gm["order"]:
+        data = [oracle.rand_buffer(L) for _ in range(K)]
+        bufs = [dev(d) for d in data] + [torch.zeros(L, dtype=torch.uint8, device=DEV)
+                                         for _ in range(2)]
+        assert ec.pq_gen(bufs, L) == 0
+        pq = np.fromfile(os.path.join(golden["_dir"], gm["scenarios"][name]["pq_file"]), np.uint8)
+        got = np.concatenate([host(bufs[K]), host(bufs[K + 1])])
+        assert (got == pq).all(), name
+        assert ec.pq_check(bufs, L) == 0
+        bufs[K + 1][17] ^= 1
+        assert ec.pq_check(bufs, L) == 1
+
+
+def test_xor_gen_raid5_shapes(ec, golden):
+    """raid5.c:188-201 in-place {from,to,to}, and raid5_simple k+1 over the
+    raid5_ut_ref known-answer pattern."""
+    for c in golden["raid5_ut_ref"]:
+        n, bl, skb = c["n"], c["blocklen"], c["strip_kb"]
+        strip = skb * 1024 // bl
+        k, S = n - 1, strip * bl
+        buf = oracle.ut_ref_pattern(strip * k, bl)
+        ref = np.fromfile(os.path.join(golden["_dir"], c["parity_file"]), np.uint8)
+        data = [dev(buf[j * S:(j + 1) * S]) for j in range(k)]
+        par = torch.zeros(S, dtype=torch.uint8, device=DEV)
+        assert ec.xor_gen(data + [par], S) == 0
+        assert (host(par) == ref).all()
+        assert ec.xor_check(data + [par], S) == 0
+        acc = torch.zeros(S, dtype=torch.uint8, device=DEV)  # memset + k xor_buf passes
+        for d in data:
+            assert ec.xor_gen([d, acc, acc], S) == 0
+        assert (host(acc) == ref).all()
+        par[3] ^= 0x40
+        assert ec.xor_check(data + [par], S) == 1
+
+
+@pytest.mark.parametrize("L", [1, 15, 16, 17, 255, 4095, 4097, 65536 + 3])
+@pytest.mark.parametrize("off", [0, 1, 8])
+def test_xor_gen_ragged_and_unaligned(ec, L, off):
+    rng = np.random.default_rng(L + off)
+    k = 5
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    big = torch.zeros((k + 1) * (L + 64) + 64, dtype=torch.uint8, device=DEV)
+    views = [big[off + j * (L + 64): off + j * (L + 64) + L] for j in range(k + 1)]
+    for j in range(k):
+        views[j].copy_(dev(data[j]))
+    assert ec.xor_gen(views, L) == 0
+    ref = np.zeros(L, np.uint8)
+    assert oracle.xor_gen(data + [ref], L) == 0
+    assert (host(views[k]) == ref).all()
+    # bytes around the destination are untouched
+    assert host(big[off + k * (L + 64) + L: off + k * (L + 64) + L + 64]).sum() == 0
+
+
+def test_isal_argument_rejection(ec):
+    t = [torch.zeros(64, dtype=torch.uint8, device=DEV) for _ in range(4)]
+    assert ec.xor_gen(t[:2], 64) == 1
+    assert ec.pq_gen(t[:3], 64) == 1
+    assert ec.pq_gen(t, 48) == 1
+    assert ec.gf_vect_mul(40, ec.gf_vect_mul_init(3), t[0], t[1]) == 1
+    assert ec.recover(2, 2, 64, t, [0, 0]) == 1
+    assert ec.recover(2, 2, 64, t, [0, 4]) == 1
+
+
+def test_gf_vect_mul_every_constant(ec):
+    L = 4096 + 32
+    rng = np.random.default_rng(7)
+    src_np = rng.integers(0, 256, L, dtype=np.uint8)
+    src_np[:256] = np.arange(256)
+    src = dev(src_np)
+    dst = torch.zeros(L, dtype=torch.uint8, device=DEV)
+    ref = np.zeros(L, np.uint8)
+    for c in range(256):
+        tbl = ec.gf_vect_mul_init(c)
+        assert ec.gf_vect_mul(L, tbl, src, dst) == 0
+        assert oracle.gf_vect_mul(L, np.frombuffer(tbl, np.uint8).copy(), src_np, ref) == 0
+        assert (host(dst) == ref).all(), c
+    # unaligned source/destination
+    s2 = torch.zeros(L + 8, dtype=torch.uint8, device=DEV)
+    s2[3:3 + L].copy_(src)
+    d2 = torch.zeros(L + 8, dtype=torch.uint8, device=DEV)
+    assert ec.gf_vect_mul(L, ec.gf_vect_mul_init(0x8E), s2[3:3 + L], d2[5:5 + L]) == 0
+    oracle.gf_vect_mul(L, oracle.gf_vect_mul_init(0x8E), src_np, ref)
+    assert (host(d2[5:5 + L]) == ref).all()
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 1), (8, 2), (9, 2), (14, 2), (16, 2), (40, 2)])
+def test_recover_every_failure_set(ec, k, m):
+    L = 4096
+    rng = np.random.default_rng(k)
+    data = np.zeros((k + m, L), np.uint8)
+    data[:k] = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    ref = oracle_encode(data[None], k, m)[0]
+    bufs = [dev(data[j]) for j in range(k + m)]
+    rc = ec.xor_gen(bufs, L) if m == 1 else ec.pq_gen(bufs, L)
+    assert rc == 0
+    assert all((host(bufs[j]) == ref[j]).all() for j in range(k + m))
+    sets = [f for nf in range(1, m + 1) for f in itertools.combinations(range(k + m), nf)]
+    if len(sets) > 200:
+        sets = sets[:: max(1, len(sets) // 200)] + [(0, 1), (k - 2, k - 1), (0, k), (k - 1, k + 1),
+                                                    (k, k + 1)]
+    for fail in sets:
+        for f in fail:
+            bufs[f].fill_(0xA5)
+        assert ec.recover(k, m, L, bufs, list(fail)) == 0
+        for j in range(k + m):
+            assert (host(bufs[j]) == ref[j]).all(), (fail, j)
+
+
+# ------------------------------------------------------------ batched API
+
+CONFIGS = [  # (k, m, strip bytes, stripes) -- BASELINE.json configs at reduced batch
+    (4, 1, 65536, 64),
+    (8, 2, 65536, 64),
+    (8, 2, 131072, 32),
+    (16, 2, 262144, 16),
+    (14, 2, 4096, 33),
+    (11, 2, 4096 + 48, 7),   # runtime-k kernel, ragged length
+    (6, 1, 1000, 5),         # ragged length, odd size
+]
+
+
+@pytest.mark.parametrize("k,m,L,B", CONFIGS)
+def test_batched_encode_vs_oracle(ec, k, m, L, B):
+    b = Batch(k, m, L, B, gap=256, seed=k * 1000 + L)
+    before = host(b.strips())
+    assert ec.encode(b.batch(ec), torch.cuda.current_stream().cuda_stream) == 0
+    sync()
+    got = host(b.strips())
+    ref = oracle_encode(before, k, m)
+    assert (got == ref).all()
+    assert (host(b.view()[:, :, L:]) == 0).all()  # gaps untouched
+
+
+def _random_failures(rng, B, k, m):
+    f = np.full((B, 2), 0xFF, np.uint8)
+    for s in range(B):
+        kind = rng.integers(0, 6)
+        if m == 1 or kind == 0:
+            f[s, 0] = rng.integers(0, k + m)
+        elif kind <= 2:
+            f[s] = rng.choice(k, 2, replace=False)
+        elif kind == 3:
+            f[s] = [rng.integers(0, k), k]
+        elif kind == 4:
+            f[s] = [k + 1, rng.integers(0, k)]
+        else:
+            f[s] = [k, k + 1]
+    return f
+
+
+@pytest.mark.parametrize("k,m,L,B", CONFIGS)
+def test_batched_reconstruct_vs_oracle(ec, k, m, L, B):
+    rng = np.random.default_rng(B + k)
+    b = Batch(k, m, L, B, seed=L + k)
+    stream = torch.cuda.current_stream().cuda_stream
+    assert ec.encode(b.batch(ec), stream) == 0
+    sync()
+    good = host(b.strips())
+    fail = _random_failures(rng, B, k, m)
+    v = b.strips()
+    for s in range(B):
+        for f in fail[s]:
+            if f != 0xFF:
+                v[s, int(f)].fill_(0x3C)
+    erased = host(b.strips())
+    # the oracle regenerates the same strips from the same erased stripes
+    ref = erased.copy()
+    assert oracle.recover_strided(ref.reshape(-1), k, m, L, B, L, (k + m) * L, fail.reshape(-1)) == 0
+    assert (ref == good).all()
+    assert ec.reconstruct(b.batch(ec), dev(fail.reshape(-1)), stream) == 0
+    sync()
+    assert (host(b.strips()) == good).all()
+
+
+def test_reconstruct_ignores_unrecoverable(ec):
+    k, m, L, B = 4, 1, 4096, 3
+    b = Batch(k, m, L, B)
+    stream = torch.cuda.current_stream().cuda_stream
+    ec.encode(b.batch(ec), stream)
+    sync()
+    v = b.strips()
+    v[1, 0].fill_(7)
+    v[1, 2].fill_(7)
+    before = host(b.strips())
+    fail = np.array([0xFF, 0xFF, 0, 2, 9, 0xFF], np.uint8)  # none, too many, out of range
+    assert ec.reconstruct(b.batch(ec), dev(fail), stream) == 0
+    sync()
+    assert (host(b.strips()) == before).all()
+
+
+def test_unaligned_batch(ec):
+    k, m, L, B = 8, 2, 4096 + 5, 4
+    b = Batch(k, m, L, B, gap=3, offset=1)
+    before = host(b.strips())
+    stream = torch.cuda.current_stream().cuda_stream
+    assert ec.encode(b.batch(ec), stream) == 0
+    sync()
+    assert (host(b.strips()) == oracle_encode(before, k, m)).all()
+    good = host(b.strips())
+    fail = np.array([[1, 6], [0, k], [k + 1, 3], [2, 0xFF]], np.uint8)
+    for s in range(B):
+        for f in fail[s]:
+            if f != 0xFF:
+                b.strips()[s, int(f)].fill_(0)
+    assert ec.reconstruct(b.batch(ec), dev(fail.reshape(-1)), stream) == 0
+    sync()
+    assert (host(b.strips()) == good).all()
+
+
+def test_stream_api(ec):
+    k, m, L, B = 8, 2, 65536, 512
+    b = Batch(k, m, L, B)
+    s = ec.stream_create()
+    try:
+        torch.cuda.synchronize()
+        assert ec.encode(b.batch(ec), s) == 0
+        assert ec.stream_query(s) in (0, 1)
+        ec.stream_synchronize(s)
+        assert ec.stream_query(s) == 0
+    finally:
+        ec.stream_destroy(s)
+    idx = [0, 77, 511]
+    got = host(b.strips()[idx])
+    ref = oracle_encode(got, k, m)
+    assert (got == ref).all()
+
+
+# ------------------------------------------------------------ BASELINE sizes
+
+@pytest.mark.parametrize("k,m,L,B", [(4, 1, 65536, 4096), (8, 2, 65536, 4096),
+                                     (8, 2, 131072, 4096), (16, 2, 262144, 1024)])
+def test_full_size_roundtrip(ec, k, m, L, B):
+    """Encode the BASELINE-sized batch, check sampled stripes against the oracle,
+    erase per-stripe failures, reconstruct, and require the original bytes back."""
+    rng = np.random.default_rng(L + k)
+    b = Batch(k, m, L, B, seed=99)
+    stream = torch.cuda.current_stream().cuda_stream
+    assert ec.encode(b.batch(ec), stream) == 0
+    sync()
+    sample = sorted(set(rng.integers(0, B, 24).tolist()) | {0, B - 1})
+    got = host(b.strips()[sample])
+    assert (got == oracle_encode(got, k, m)).all()
+    good = b.strips().clone()
+    fail = _random_failures(rng, B, k, m)
+    fd = dev(fail.reshape(-1))
+    # erase on the device: overwrite each failed strip
+    v = b.strips()
+    for slot in range(2):
+        idx = np.nonzero(fail[:, slot] != 0xFF)[0]
+        si = torch.from_numpy(idx).to(DEV)
+        ji = torch.from_numpy(fail[idx, slot].astype(np.int64)).to(DEV)
+        v[si, ji] = 0x77
+    assert ec.reconstruct(b.batch(ec), fd, stream) == 0
+    sync()
+    assert torch.equal(b.strips(), good)
