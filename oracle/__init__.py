@@ -58,6 +58,8 @@ def lib() -> C.CDLL:
         L.orc_raid5_start_geometry.argtypes = [i32, i32, C.c_uint64, u32, P64, P64, P64, P64]
         L.orc_srand.argtypes = [C.c_uint]
         L.orc_rand_buffer.argtypes = [vp, C.c_long]
+        L.orc_glibc_srand.argtypes = [C.c_uint]
+        L.orc_glibc_rand_buffer.argtypes = [vp, C.c_long]
         L.orc_fill_splitmix.argtypes = [vp, sz, C.c_uint64]
         L.orc_fill_ut_ref_pattern.argtypes = [vp, C.c_uint64, u32]
         _lib = L
@@ -154,6 +156,16 @@ def srand(seed: int) -> None:
 def rand_buffer(n: int) -> np.ndarray:
     b = np.zeros(n, np.uint8)
     lib().orc_rand_buffer(b.ctypes.data, n)
+    return b
+
+
+def glibc_srand(seed: int) -> None:
+    lib().orc_glibc_srand(seed)
+
+
+def glibc_rand_buffer(n: int) -> np.ndarray:
+    b = np.zeros(n, np.uint8)
+    lib().orc_glibc_rand_buffer(b.ctypes.data, n)
     return b
 
 

@@ -168,6 +168,34 @@ int orc_pq_gen(int vects, int len, void **array)
     return 0;
 }
 
+/* P+Q over any length (the batched API has no isa-l length contract):
+ * 8-byte words, then a bytewise tail. */
+static void pq_any(int k, size_t len, unsigned char **v)
+{
+    size_t w = 0;
+    for (; w + 8 <= len; w += 8) {
+        uint64_t p, q, s;
+        memcpy(&s, v[k - 1] + w, 8);
+        p = q = s;
+        for (int j = k - 2; j >= 0; j--) {
+            memcpy(&s, v[j] + w, 8);
+            p ^= s;
+            q = mul2_u64(q) ^ s;
+        }
+        memcpy(v[k] + w, &p, 8);
+        memcpy(v[k + 1] + w, &q, 8);
+    }
+    for (; w < len; w++) {
+        unsigned char p = v[k - 1][w], q = p;
+        for (int j = k - 2; j >= 0; j--) {
+            p ^= v[j][w];
+            q = (unsigned char)(mul2_u8(q) ^ v[j][w]);
+        }
+        v[k][w] = p;
+        v[k + 1][w] = q;
+    }
+}
+
 /* xor_check: 0 iff XOR over all vects (including the parity) is zero. */
 int orc_xor_check(int vects, int len, void **array)
 {
@@ -339,10 +367,16 @@ int orc_encode_strided(int k, int m, size_t len, uint32_t nstripes,
         return -1;
     for (uint32_t s = 0; s < nstripes; s++) {
         strided_ptrs(k, m, base, strip_stride, stripe_stride, s, ptrs);
-        int rc = (m == 1) ? orc_xor_gen(k + 1, (int)len, ptrs)
-                          : orc_pq_gen(k + 2, (int)len, ptrs);
-        if (rc)
-            return rc;
+        if (m == 1) {
+            int rc = orc_xor_gen(k + 1, (int)len, ptrs);
+            if (rc)
+                return rc;
+        } else if (k == 1) {
+            memcpy(ptrs[1], ptrs[0], len); /* P = Q = D_0 */
+            memcpy(ptrs[2], ptrs[0], len);
+        } else {
+            pq_any(k, len, (unsigned char **)ptrs);
+        }
     }
     return 0;
 }
@@ -470,10 +504,33 @@ void orc_raid5_start_geometry(int num_base_bdevs, int max_degraded, uint64_t min
 
 /* ---------------------------------------------------------- generators */
 
-void orc_srand(unsigned int seed) { srand(seed); }
+/* glibc's rand() is random() on the default 128-byte TYPE_3 state; a private
+ * random_r state of the same size yields the identical sequence without being
+ * disturbed by other threads of the process (the HIP runtime, torch) that also
+ * draw from the global rand() state. */
+static struct random_data g_rd;
+static char g_rstate[128];
+
+void orc_srand(unsigned int seed)
+{
+    memset(&g_rd, 0, sizeof(g_rd));
+    initstate_r(seed, g_rstate, sizeof(g_rstate), &g_rd);
+}
 
 /* gf_vect_mul.c:21-26: buf[i] = rand() truncated to a byte. */
 void orc_rand_buffer(unsigned char *buf, long size)
+{
+    for (long i = 0; i < size; i++) {
+        int32_t r;
+        random_r(&g_rd, &r);
+        buf[i] = (unsigned char)r;
+    }
+}
+
+/* The same, straight from glibc's global rand() (only for cross-checking the
+ * private-state generator in a quiet process). */
+void orc_glibc_srand(unsigned int seed) { srand(seed); }
+void orc_glibc_rand_buffer(unsigned char *buf, long size)
 {
     for (long i = 0; i < size; i++)
         buf[i] = (unsigned char)rand();

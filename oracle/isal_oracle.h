@@ -76,8 +76,10 @@ void orc_raid5_start_geometry(int num_base_bdevs, int max_degraded, uint64_t min
                               uint64_t *optimal_io_boundary);
 
 /* ---- input generators ---- */
-void orc_srand(unsigned int seed);                         /* glibc srand */
+void orc_srand(unsigned int seed);                         /* glibc srand, private state */
 void orc_rand_buffer(unsigned char *buf, long size);      /* gf_vect_mul.c:21-26 */
+void orc_glibc_srand(unsigned int seed);                   /* global glibc srand */
+void orc_glibc_rand_buffer(unsigned char *buf, long size); /* global glibc rand */
 uint64_t orc_splitmix64(uint64_t *state);
 void orc_fill_splitmix(uint8_t *buf, size_t len, uint64_t seed);
 void orc_fill_ut_ref_pattern(uint8_t *buf, uint64_t num_blocks, uint32_t blocklen);

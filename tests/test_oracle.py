@@ -151,6 +151,15 @@ def test_raid5_ut_ref_known_answer(golden, case):
     assert (par == np.fromfile(os.path.join(golden["_dir"], c["parity_file"]), np.uint8)).all()
 
 
+def test_private_rand_state_matches_glibc_rand():
+    """orc_srand/orc_rand_buffer (random_r, private state) == srand/rand."""
+    oracle.glibc_srand(0x1234)
+    a = oracle.glibc_rand_buffer(3 * 4096)
+    oracle.srand(0x1234)
+    b = oracle.rand_buffer(3 * 4096)
+    assert (a == b).all()
+
+
 def test_raid5_geometry_grid():
     """raid5_ut.c:61-105 parameter grid and :176-195 assertions."""
     for n in (3, 4, 5):
