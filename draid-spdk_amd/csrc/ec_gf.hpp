@@ -76,30 +76,31 @@ __host__ __device__ __forceinline__ uint32_t mul2_byte(uint32_t c)
     return ((c << 1) ^ ((c & 0x80u) ? 0x1du : 0u)) & 0xffu;
 }
 
+// Closed form: with p_b = c * 2^b, word w of the low table holds entries
+// 4w..4w+3 = base_w ^ {0, p0, p1, p0^p1}, base_w = (w&1 ? p2 : 0) ^ (w&2 ? p3 : 0);
+// the high table is the same over p4..p7.  ~30 scalar ops for both halves (the
+// constant is wave-uniform, so this runs on the SALU).
+__host__ __device__ __forceinline__ void nib_words(uint32_t p0, uint32_t p1, uint32_t p2,
+                                                       uint32_t p3, uint32_t w[4])
+{
+    const uint32_t t = (p0 << 8) | (p1 << 16) | ((p0 ^ p1) << 24);
+    w[0] = t;
+    w[1] = t ^ (p2 * 0x01010101u);
+    w[2] = t ^ (p3 * 0x01010101u);
+    w[3] = t ^ ((p2 ^ p3) * 0x01010101u);
+
+}
+
 __host__ __device__ inline NibTable make_nib_table(uint32_t c)
 {
     uint32_t p[8];  // c * 2^i
     p[0] = c & 0xffu;
+#pragma unroll
     for (int i = 1; i < 8; ++i)
         p[i] = mul2_byte(p[i - 1]);
-    NibTable t{};
-    for (int w = 0; w < 4; ++w) {
-        uint32_t lo = 0, hi = 0;
-        for (int b = 0; b < 4; ++b) {
-            const int n = 4 * w + b;
-            uint32_t vl = 0, vh = 0;
-            for (int bit = 0; bit < 4; ++bit) {
-                if (n & (1 << bit)) {
-                    vl ^= p[bit];
-                    vh ^= p[bit + 4];
-                }
-            }
-            lo |= vl << (8 * b);
-            hi |= vh << (8 * b);
-        }
-        t.lo[w] = lo;
-        t.hi[w] = hi;
-    }
+    NibTable t;
+    nib_words(p[0], p[1], p[2], p[3], t.lo);
+    nib_words(p[4], p[5], p[6], p[7], t.hi);
     return t;
 }
 

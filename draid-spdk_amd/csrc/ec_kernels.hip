@@ -125,7 +125,7 @@ __device__ __forceinline__ void for_sources_desc(int k, F&& f)
 // either stores them (CHECK == false) or compares them with the stored parity.
 // BOUNDED == false: the caller guarantees every element is in range (full
 // chunks), so no load or store is predicated.
-template <int KT, int M, int U, bool NT, bool CHECK, bool BOUNDED, class W, class Ptrs>
+template <int KT, int M, int U, int POL, bool CHECK, bool BOUNDED, class W, class Ptrs>
 __device__ __forceinline__ bool encode_elems(const Ptrs& pp, uint32_t s, int k, uint32_t i0,
                                              uint32_t stride, uint32_t n)
 {
@@ -142,7 +142,7 @@ __device__ __forceinline__ bool encode_elems(const Ptrs& pp, uint32_t s, int k, 
         const uint8_t* src = pp.get(s, j);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const W d = ok[u] ? MW::template ld<NT>(src, i0 + u * stride) : W(0);
+            const W d = ok[u] ? MW::template ld<(POL & 1) != 0>(src, i0 + u * stride) : W(0);
             p[u] ^= d;
             if constexpr (M == 2)
                 q[u] = gf_mul2(q[u]) ^ d;
@@ -161,9 +161,9 @@ __device__ __forceinline__ bool encode_elems(const Ptrs& pp, uint32_t s, int k, 
             if constexpr (M == 2)
                 bad |= MW::any(MW::template ld<false>(dq, i) ^ q[u]);
         } else {
-            MW::template st<NT>(dp, i, p[u]);
+            MW::template st<(POL & 2) != 0>(dp, i, p[u]);
             if constexpr (M == 2)
-                MW::template st<NT>(dq, i, q[u]);
+                MW::template st<(POL & 2) != 0>(dq, i, q[u]);
         }
     }
     return bad;
@@ -184,30 +184,71 @@ __device__ __forceinline__ bool stripe_aligned(const Ptrs& pp, uint32_t s, int k
     return (acc & 15u) == 0;
 }
 
-template <int KT, int M, int U, bool NT, bool CHECK, class Ptrs>
-__global__ __launch_bounds__(kThreads) void k_encode(Ptrs pp, uint32_t k_rt, uint32_t len,
-                                                     uint32_t cps, uint32_t* flag)
+// Launch configuration knobs (A/B-tested with tools/sweep.py):
+//   NTHR  lanes per workgroup           U    16-B vectors per lane per strip
+//   POL   bit0 nt loads, bit1 nt stores
+//   MAP   0: block b -> (stripe b / cps, chunk b % cps)
+//         1: chunk-major (chunk b / nstripes, stripe b % nstripes)
+//         2: persistent grid-stride over stripe-major items
+//   PLAN  (reconstruct) 0: exp/log tables staged in LDS, 1: scalar reads of
+//         the __constant__ tables (no LDS, no barrier)
+template <int NTHR_, int U_, int POL_, int MAP_, int PLAN_ = 0>
+struct Cfg {
+    static constexpr int NTHR = NTHR_, U = U_, POL = POL_, MAP = MAP_, PLAN = PLAN_;
+};
+
+template <class C>
+__device__ __forceinline__ void item_coords(uint32_t b, uint32_t cps, uint32_t nstripes,
+                                            uint32_t& s, uint32_t& c)
 {
-    const uint32_t s = blockIdx.x / cps;
-    const uint32_t c = blockIdx.x - s * cps;
-    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
-    constexpr uint32_t EPB = static_cast<uint32_t>(kThreads) * U;  // vectors per block
+    if constexpr (C::MAP == 1) {
+        c = b / nstripes;
+        s = b - c * nstripes;
+    } else {
+        s = b / cps;
+        c = b - s * cps;
+    }
+}
+
+// One work item = chunk c (NTHR*U vectors) of every strip of stripe s.
+template <int KT, int M, bool CHECK, class C, class Ptrs>
+__device__ __forceinline__ bool encode_item(const Ptrs& pp, uint32_t s, uint32_t c, int k,
+                                            uint32_t len, uint32_t cps)
+{
+    constexpr int NTHR = C::NTHR, U = C::U, POL = C::POL;
+    constexpr uint32_t EPB = static_cast<uint32_t>(NTHR) * U;  // vectors per item
     const uint32_t nvec = len >> 4;
     bool bad = false;
     if (stripe_aligned<KT, M>(pp, s, k)) {
         const uint32_t i0 = c * EPB + threadIdx.x;
         if ((c + 1) * EPB <= nvec)
-            bad = encode_elems<KT, M, U, NT, CHECK, false, u32x4>(pp, s, k, i0, kThreads, nvec);
+            bad = encode_elems<KT, M, U, POL, CHECK, false, u32x4>(pp, s, k, i0, NTHR, nvec);
         else
-            bad = encode_elems<KT, M, U, NT, CHECK, true, u32x4>(pp, s, k, i0, kThreads, nvec);
+            bad = encode_elems<KT, M, U, POL, CHECK, true, u32x4>(pp, s, k, i0, NTHR, nvec);
         const uint32_t tail = len & 15u;
         if (tail && c == cps - 1 && threadIdx.x < tail)
-            bad |= encode_elems<0, M, 1, false, CHECK, true, uint32_t>(
-                pp, s, k, nvec * 16 + threadIdx.x, kThreads, len);
+            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(
+                pp, s, k, nvec * 16 + threadIdx.x, NTHR, len);
     } else {
         const uint32_t b1 = min(len, (c + 1) * EPB * 16);
-        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += kThreads)
-            bad |= encode_elems<0, M, 1, false, CHECK, true, uint32_t>(pp, s, k, b, kThreads, b1);
+        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += NTHR)
+            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(pp, s, k, b, NTHR, b1);
+    }
+    return bad;
+}
+
+template <int KT, int M, bool CHECK, class C, class Ptrs>
+__global__ __launch_bounds__(C::NTHR) void k_encode(Ptrs pp, uint32_t k_rt, uint32_t len,
+                                                    uint32_t cps, uint32_t nstripes,
+                                                    uint32_t* flag)
+{
+    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
+    const uint32_t total = cps * nstripes;
+    bool bad = false;
+    for (uint32_t b = blockIdx.x; b < total; b += (C::MAP == 2 ? gridDim.x : total)) {
+        uint32_t s, c;
+        item_coords<C>(b, cps, nstripes, s, c);
+        bad |= encode_item<KT, M, CHECK, C>(pp, s, c, k, len, cps);
     }
     if constexpr (CHECK) {
         if (bad)
@@ -224,14 +265,13 @@ struct RecPlan {
     bool lostP, lostQ; // parity strips to regenerate
     bool needq;        // the Q syndrome over the survivors is needed
     bool skip;         // unrecoverable / nothing to do
-    NibTable t1, t2;   // constant multipliers (see build_plan)
+    NibTable t1, t2;   // constant multipliers (see plan_constants)
 };
 
-// Decodes the failure pair and derives the GF constants from the exp/log
-// tables staged in LDS (gf_vect_mul.c:296-326 for the D+D constants).
+// Decodes the (wave-uniform) failure pair: which strips are lost, which
+// syndromes are needed.  No table lookups -- runs before any load is issued.
 template <int M>
-__device__ __forceinline__ RecPlan build_plan(int k, uint32_t f0, uint32_t f1, const uint8_t* s_exp,
-                                              const uint8_t* s_log)
+__device__ __forceinline__ RecPlan decode_failures(int k, uint32_t f0, uint32_t f1)
 {
     RecPlan pl;
     pl.x = -1;
@@ -239,7 +279,8 @@ __device__ __forceinline__ RecPlan build_plan(int k, uint32_t f0, uint32_t f1, c
     pl.nd = 0;
     pl.lostP = false;
     pl.lostQ = false;
-    const uint32_t f[2] = {f0, f1};
+    const uint32_t f[2] = {static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(f0)),
+                           static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(f1))};
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int j = static_cast<int>(f[t]);
@@ -267,25 +308,39 @@ __device__ __forceinline__ RecPlan build_plan(int k, uint32_t f0, uint32_t f1, c
     const int nf = pl.nd + (pl.lostP ? 1 : 0) + (pl.lostQ ? 1 : 0);
     pl.skip = (nf == 0) || (nf > M);
     pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
-    uint32_t c1 = 0, c2 = 0;
-    if (pl.nd == 1 && !pl.lostP && pl.lostQ) {
-        c1 = s_exp[pl.x];                       // Q = Qs ^ 2^x D_x
-    } else if (pl.nd == 1 && pl.lostP) {
-        c1 = s_exp[255 - pl.x];                 // D_x = 2^-x (Q ^ Qs)
-    } else if (pl.nd == 2) {
-        const uint32_t gyx = s_exp[pl.y - pl.x];
-        const uint32_t den = s_exp[255 - s_log[gyx ^ 1u]];           // 1 / (2^(y-x) ^ 1)
-        c1 = s_exp[s_log[gyx] + s_log[den]];                         // A = 2^(y-x) / (...)
-        c2 = s_exp[(255 - pl.x) + s_log[den]];                       // B = 2^-x / (...)
-    }
-    pl.t1 = make_nib_table(c1);
-    pl.t2 = make_nib_table(c2);
     return pl;
 }
 
-template <int KT, int M, int U, bool NT, bool BOUNDED, class W, class Ptrs>
-__device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k, const RecPlan& pl,
-                                              uint32_t i0, uint32_t stride, uint32_t n)
+// GF constants of the plan from exp/log tables (gf_vect_mul.c:255-268 for
+// 2^-x, :296-326 for the D+D constants A and B).
+__device__ __forceinline__ void plan_constants(RecPlan& pl, const uint8_t* t_exp,
+                                               const uint8_t* t_log)
+{
+    uint32_t c1 = 0, c2 = 0;
+    if (pl.nd == 1 && !pl.lostP && pl.lostQ) {
+        c1 = t_exp[pl.x];                                   // Q = Qs ^ 2^x D_x
+    } else if (pl.nd == 1 && pl.lostP) {
+        c1 = t_exp[255 - pl.x];                             // D_x = 2^-x (Q ^ Qs)
+    } else if (pl.nd == 2) {
+        const uint32_t gyx = t_exp[pl.y - pl.x];
+        const uint32_t den = t_exp[255 - t_log[gyx ^ 1u]];  // 1 / (2^(y-x) ^ 1)
+        c1 = t_exp[t_log[gyx] + t_log[den]];                // A = 2^(y-x) / (...)
+        c2 = t_exp[(255 - pl.x) + t_log[den]];              // B = 2^-x / (...)
+    }
+    // Wave-uniform (one stripe per workgroup): the table build runs on the SALU.
+    c1 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c1));
+    c2 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c2));
+    pl.t1 = make_nib_table(c1);
+    pl.t2 = make_nib_table(c2);
+}
+
+// Loads and syndrome accumulation for U elements, then `constants(pl)` (which
+// may stage tables and hit a workgroup barrier -- every lane calls it exactly
+// once, after its loads are in flight), then the outputs.
+template <int KT, int M, int U, int POL, bool BOUNDED, class W, class Ptrs, class F>
+__device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k, RecPlan& pl,
+                                              uint32_t i0, uint32_t stride, uint32_t n,
+                                              F&& constants)
 {
     using MW = Mem<W>;
     const uint8_t* pP = pp.get(s, k);
@@ -302,8 +357,8 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
         ok[u] = !BOUNDED || i0 + u * stride < n;
         ps[u] = W(0);
         qs[u] = W(0);
-        pv[u] = ok[u] ? MW::template ld<NT>(pl.lostP ? sub : pP, i0 + u * stride) : W(0);
-        qv[u] = ok[u] ? MW::template ld<NT>(useQ ? pQ : sub, i0 + u * stride) : W(0);
+        pv[u] = ok[u] ? MW::template ld<(POL & 1) != 0>(pl.lostP ? sub : pP, i0 + u * stride) : W(0);
+        qv[u] = ok[u] ? MW::template ld<(POL & 1) != 0>(useQ ? pQ : sub, i0 + u * stride) : W(0);
     }
     for_sources_desc<KT>(k, [&](int j) {
         const bool dead = (j == pl.x) || (j == pl.y);
@@ -311,12 +366,13 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
         const uint32_t keep = dead ? 0u : 0xffffffffu;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const W d = (ok[u] ? MW::template ld<NT>(src, i0 + u * stride) : W(0)) & keep;
+            const W d = (ok[u] ? MW::template ld<(POL & 1) != 0>(src, i0 + u * stride) : W(0)) & keep;
             ps[u] ^= d;
             if constexpr (M == 2)
                 qs[u] = gf_mul2(qs[u]) ^ d;
         }
     });
+    constants(pl);
     const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
     const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
 #pragma unroll
@@ -326,71 +382,109 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
         const uint32_t i = i0 + u * stride;
         if (pl.nd == 0) {
             if (pl.lostP)
-                MW::template st<NT>(pP, i, ps[u]);
+                MW::template st<(POL & 2) != 0>(pP, i, ps[u]);
             if (M == 2 && pl.lostQ)
-                MW::template st<NT>(pQ, i, qs[u]);
+                MW::template st<(POL & 2) != 0>(pQ, i, qs[u]);
         } else if (pl.nd == 1) {
             if (!pl.lostP) {
                 const W dx = pv[u] ^ ps[u];
-                MW::template st<NT>(pX, i, dx);
+                MW::template st<(POL & 2) != 0>(pX, i, dx);
                 if (M == 2 && pl.lostQ)
-                    MW::template st<NT>(pQ, i, qs[u] ^ gf_mulc(pl.t1, dx));
+                    MW::template st<(POL & 2) != 0>(pQ, i, qs[u] ^ gf_mulc(pl.t1, dx));
             } else {
                 const W dx = gf_mulc(pl.t1, qv[u] ^ qs[u]);
-                MW::template st<NT>(pX, i, dx);
-                MW::template st<NT>(pP, i, ps[u] ^ dx);
+                MW::template st<(POL & 2) != 0>(pX, i, dx);
+                MW::template st<(POL & 2) != 0>(pP, i, ps[u] ^ dx);
             }
         } else {
             const W pxy = pv[u] ^ ps[u];
             const W qxy = qv[u] ^ qs[u];
             const W dx = gf_mulc(pl.t1, pxy) ^ gf_mulc(pl.t2, qxy);
-            MW::template st<NT>(pX, i, dx);
-            MW::template st<NT>(pY, i, pxy ^ dx);
+            MW::template st<(POL & 2) != 0>(pX, i, dx);
+            MW::template st<(POL & 2) != 0>(pY, i, pxy ^ dx);
         }
     }
 }
 
-template <int KT, int M, int U, bool NT, class Ptrs>
-__global__ __launch_bounds__(kThreads) void k_reconstruct(Ptrs pp, uint32_t k_rt, uint32_t len,
-                                                          uint32_t cps, const uint8_t* fail,
-                                                          uint32_t f01)
-{
-    // LDS-staged exp/log tables (768 B) for the per-stripe constants.
-    __shared__ uint32_t s_tab[(512 + 256) / 4];
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(&c_gf);
-    for (int t = threadIdx.x; t < (512 + 256) / 4; t += kThreads)
-        s_tab[t] = g[t];
-    __syncthreads();
-    const uint8_t* s_exp = reinterpret_cast<const uint8_t*>(s_tab);
-    const uint8_t* s_log = s_exp + 512;
+// LDS image of the exp/log tables (768 B).
+struct LdsGf {
+    uint32_t w[(512 + 256) / 4];
+};
 
-    const uint32_t s = blockIdx.x / cps;
-    const uint32_t c = blockIdx.x - s * cps;
-    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
-    uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
-    if (fail) {
-        f0 = fail[2 * (size_t)s];
-        f1 = fail[2 * (size_t)s + 1];
-    }
-    const RecPlan pl = build_plan<M>(k, f0, f1, s_exp, s_log);
-    if (pl.skip)
-        return;
-    constexpr uint32_t EPB = static_cast<uint32_t>(kThreads) * U;
+template <int NTHR>
+__device__ __forceinline__ void stage_gf_tables(LdsGf& lds)
+{
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(&c_gf);
+    for (int t = threadIdx.x; t < (512 + 256) / 4; t += NTHR)
+        lds.w[t] = g[t];
+    __syncthreads();
+}
+
+template <int KT, int M, class C, class Ptrs, class F>
+__device__ __forceinline__ void reconstruct_item(const Ptrs& pp, uint32_t s, uint32_t c, int k,
+                                                 uint32_t len, uint32_t cps, RecPlan& pl,
+                                                 F&& constants)
+{
+    constexpr int NTHR = C::NTHR, U = C::U, POL = C::POL;
+    constexpr uint32_t EPB = static_cast<uint32_t>(NTHR) * U;
     const uint32_t nvec = len >> 4;
+    auto none = [](RecPlan&) {};
     if (stripe_aligned<KT, M>(pp, s, k)) {
         const uint32_t i0 = c * EPB + threadIdx.x;
         if ((c + 1) * EPB <= nvec)
-            recover_elems<KT, M, U, NT, false, u32x4>(pp, s, k, pl, i0, kThreads, nvec);
+            recover_elems<KT, M, U, POL, false, u32x4>(pp, s, k, pl, i0, NTHR, nvec, constants);
         else
-            recover_elems<KT, M, U, NT, true, u32x4>(pp, s, k, pl, i0, kThreads, nvec);
+            recover_elems<KT, M, U, POL, true, u32x4>(pp, s, k, pl, i0, NTHR, nvec, constants);
         const uint32_t tail = len & 15u;
         if (tail && c == cps - 1 && threadIdx.x < tail)
-            recover_elems<0, M, 1, false, true, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
-                                                          kThreads, len);
+            recover_elems<0, M, 1, 0, true, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
+                                                      NTHR, len, none);
     } else {
+        constants(pl);
         const uint32_t b1 = min(len, (c + 1) * EPB * 16);
-        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += kThreads)
-            recover_elems<0, M, 1, false, true, uint32_t>(pp, s, k, pl, b, kThreads, b1);
+        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += NTHR)
+            recover_elems<0, M, 1, 0, true, uint32_t>(pp, s, k, pl, b, NTHR, b1, none);
+    }
+}
+
+template <int KT, int M, class C, class Ptrs>
+__global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt, uint32_t len,
+                                                         uint32_t cps, uint32_t nstripes,
+                                                         const uint8_t* fail, uint32_t f01)
+{
+    __shared__ LdsGf lds;
+    const uint8_t* l_exp = reinterpret_cast<const uint8_t*>(lds.w);
+    const uint8_t* l_log = l_exp + 512;
+    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
+    const uint32_t total = cps * nstripes;
+    if constexpr (C::MAP == 2)
+        stage_gf_tables<C::NTHR>(lds);  // once per persistent workgroup
+    for (uint32_t b = blockIdx.x; b < total; b += (C::MAP == 2 ? gridDim.x : total)) {
+        uint32_t s, c;
+        item_coords<C>(b, cps, nstripes, s, c);
+        uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
+        if (fail) {
+            f0 = fail[2 * (size_t)s];
+            f1 = fail[2 * (size_t)s + 1];
+        }
+        RecPlan pl = decode_failures<M>(k, f0, f1);
+        if (pl.skip)
+            continue;  // uniform across the workgroup
+        if constexpr (C::PLAN == 1) {
+            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
+                plan_constants(p, c_gf.exp, c_gf.log);
+            });
+        } else if constexpr (C::MAP == 2) {
+            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
+                plan_constants(p, l_exp, l_log);
+            });
+        } else {
+            // Stage the tables while this lane's strip loads are in flight.
+            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
+                stage_gf_tables<C::NTHR>(lds);
+                plan_constants(p, l_exp, l_log);
+            });
+        }
     }
 }
 
@@ -415,80 +509,160 @@ __global__ __launch_bounds__(kThreads) void k_gf_vect_mul(const uint8_t* src, ui
 
 // ------------------------------------------------------------ launchers
 
-// Vectors per lane per strip: fewer sources -> more vectors, so a lane always
-// has roughly 8-16 loads of 16 B in flight.
-constexpr int unroll_for(int k) { return k <= 4 ? 4 : (k <= 8 ? 2 : 1); }
+// Vectors per lane per strip (measured with tools/sweep.py at 8+2 x 64 KiB):
+// encode is fastest at U=1 (6.43 TB/s vs 6.20 at U=2); reconstruct at U=2
+// (6.14 vs 5.81 TB/s), where a workgroup also stages the GF tables and derives
+// its constants, so more bytes per workgroup amortise that.  Fewer sources keep
+// more vectors so a lane still issues >= 8 loads.
+constexpr int enc_unroll(int k) { return k <= 4 ? 2 : 1; }
+constexpr int rec_unroll(int k) { return k <= 8 ? 2 : 1; }
 
-static inline uint32_t chunks_per_stripe(uint64_t len, int U)
+static inline uint32_t chunks_per_stripe(uint64_t len, int nthr, int U)
 {
-    const uint64_t cb = static_cast<uint64_t>(kThreads) * U * 16;
+    const uint64_t cb = static_cast<uint64_t>(nthr) * U * 16;
     const uint64_t c = (len + cb - 1) / cb;
     return static_cast<uint32_t>(c == 0 ? 1 : c);
 }
 
-template <int KT, int M, bool NT, bool CHECK, class Ptrs>
+static int device_cus()
+{
+    static thread_local int dev = -1, cus = 0;
+    int d = 0;
+    (void)hipGetDevice(&d);
+    if (d != dev || cus <= 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        dev = d;
+    }
+    return cus;
+}
+
+template <class C>
+static bool grid_for(uint64_t len, uint32_t nstripes, uint32_t& cps, uint32_t& grid)
+{
+    cps = chunks_per_stripe(len, C::NTHR, C::U);
+    const uint64_t items = static_cast<uint64_t>(cps) * nstripes;
+    if (items > 0x7fffffffull || len > kMaxStripLen)
+        return false;
+    uint64_t g = items;
+    if constexpr (C::MAP == 2) {
+        const uint64_t resident = static_cast<uint64_t>(device_cus()) * (2048 / C::NTHR);
+        g = items < resident ? items : resident;
+    }
+    grid = static_cast<uint32_t>(g);
+    return true;
+}
+
+template <int KT, int M, bool CHECK, class C, class Ptrs>
 static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
                             uint32_t* flag, hipStream_t st)
 {
-    constexpr int U = KT > 0 ? unroll_for(KT) : 2;
-    const uint32_t cps = chunks_per_stripe(len, U);
-    const uint64_t blocks = static_cast<uint64_t>(cps) * nstripes;
-    if (blocks == 0)
+    uint32_t cps, grid;
+    if (nstripes == 0 || len == 0)
         return hipSuccess;
-    if (blocks > 0x7fffffffull || len > kMaxStripLen)
+    if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_encode<KT, M, U, NT, CHECK, Ptrs>), dim3(static_cast<uint32_t>(blocks)),
-                       dim3(kThreads), 0, st, pp, k, static_cast<uint32_t>(len), cps, flag);
+    hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp, k,
+                       static_cast<uint32_t>(len), cps, nstripes, flag);
     return hipGetLastError();
 }
 
-template <int KT, int M, bool NT, class Ptrs>
+template <int KT, int M, class C, class Ptrs>
 static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
                                  const uint8_t* fail, uint32_t f01, hipStream_t st)
 {
-    constexpr int U = KT > 0 ? unroll_for(KT) : 2;
-    const uint32_t cps = chunks_per_stripe(len, U);
-    const uint64_t blocks = static_cast<uint64_t>(cps) * nstripes;
-    if (blocks == 0)
+    uint32_t cps, grid;
+    if (nstripes == 0 || len == 0)
         return hipSuccess;
-    if (blocks > 0x7fffffffull || len > kMaxStripLen)
+    if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_reconstruct<KT, M, U, NT, Ptrs>), dim3(static_cast<uint32_t>(blocks)),
-                       dim3(kThreads), 0, st, pp, k, static_cast<uint32_t>(len), cps, fail, f01);
+    hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp, k,
+                       static_cast<uint32_t>(len), cps, nstripes, fail, f01);
     return hipGetLastError();
 }
+
+// Production configuration: 256 lanes, non-temporal loads and stores,
+// one item per workgroup, LDS-staged GF tables.
+template <int U>
+using CfgDefault = Cfg<256, U, 3, 0, 0>;
 
 // k values with a fully unrolled instantiation; others use the runtime-k loop.
 #define DRAID_FOR_EACH_K(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(12) X(14) X(16)
 
-template <int M, bool NT, class Ptrs>
+template <int M, class Ptrs>
 static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
                                   hipStream_t st)
 {
     switch (k) {
 #define DRAID_CASE(K) \
     case K:           \
-        return go_encode<K, M, NT, false>(pp, k, len, nstripes, nullptr, st);
+        return go_encode<K, M, false, CfgDefault<enc_unroll(K)>>(pp, k, len, nstripes, nullptr, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return go_encode<0, M, NT, false>(pp, k, len, nstripes, nullptr, st);
+        return go_encode<0, M, false, CfgDefault<2>>(pp, k, len, nstripes, nullptr, st);
     }
 }
 
-template <int M, bool NT, class Ptrs>
+template <int M, class Ptrs>
 static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
                                        uint32_t nstripes, const uint8_t* fail, uint32_t f01,
                                        hipStream_t st)
 {
     switch (k) {
-#define DRAID_CASE(K) \
-    case K:           \
-        return go_reconstruct<K, M, NT>(pp, k, len, nstripes, fail, f01, st);
+#define DRAID_CASE(K)                                                                       \
+    case K:                                                                                 \
+        return go_reconstruct<K, M, CfgDefault<rec_unroll(K)>>(pp, k, len, nstripes, fail, \
+                                                               f01, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return go_reconstruct<0, M, NT>(pp, k, len, nstripes, fail, f01, st);
+        return go_reconstruct<0, M, CfgDefault<2>>(pp, k, len, nstripes, fail, f01, st);
+    }
+}
+
+// A/B variants of the RAID6 8+2 batched kernels (tools/sweep.py only).
+using V1 = Cfg<256, 2, 3, 0, 0>;   // U=2
+using V2 = Cfg<512, 1, 3, 0, 0>;   // 512 lanes
+using V3 = Cfg<128, 1, 3, 0, 0>;   // 128 lanes
+using V4 = Cfg<256, 1, 3, 1, 0>;   // chunk-major block mapping
+using V5 = Cfg<256, 1, 3, 2, 0>;   // persistent grid-stride
+using V6 = Cfg<256, 1, 3, 0, 1>;   // scalar plan (no LDS / barrier)
+using V7 = Cfg<512, 1, 3, 2, 1>;   // persistent, 512 lanes, scalar plan
+using V8 = Cfg<1024, 1, 3, 0, 0>;  // 1024 lanes
+using V9 = Cfg<64, 1, 3, 0, 0>;    // one wave
+using V10 = Cfg<256, 1, 3, 0, 0>;  // U=1
+using V11 = Cfg<512, 2, 3, 0, 0>;  // 512 lanes, U=2
+using V12 = Cfg<256, 4, 3, 0, 0>;  // U=4
+#define DRAID_VARIANTS(X) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5) X(6, V6) X(7, V7) X(8, V8) \
+    X(9, V9) X(10, V10) X(11, V11) X(12, V12)
+
+static hipError_t variant_encode_8p2(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
+                                     hipStream_t st)
+{
+    switch (v) {
+#define DRAID_V(N, C) \
+    case N:           \
+        return go_encode<8, 2, false, C>(pp, 8, len, ns, nullptr, st);
+        DRAID_VARIANTS(DRAID_V)
+#undef DRAID_V
+    default:
+        return go_encode<8, 2, false, CfgDefault<enc_unroll(8)>>(pp, 8, len, ns, nullptr, st);
+    }
+}
+
+static hipError_t variant_reconstruct_8p2(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
+                                          const uint8_t* fail, hipStream_t st)
+{
+    switch (v) {
+#define DRAID_V(N, C) \
+    case N:           \
+        return go_reconstruct<8, 2, C>(pp, 8, len, ns, fail, 0xffffu, st);
+        DRAID_VARIANTS(DRAID_V)
+#undef DRAID_V
+    default:
+        return go_reconstruct<8, 2, CfgDefault<rec_unroll(8)>>(pp, 8, len, ns, fail, 0xffffu, st);
     }
 }
 
@@ -497,17 +671,16 @@ hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes
 {
     if (table) {
         const TablePtrs pp{table, k + m};
-        const bool nt = g_variant != 1;
+        if (g_variant != 0 && k == 8 && m == 2)
+            return variant_encode_8p2(g_variant, pp, len, nstripes, st);
         if (m == 1)
-            return nt ? dispatch_encode<1, true>(pp, k, len, nstripes, st)
-                      : dispatch_encode<1, false>(pp, k, len, nstripes, st);
-        return nt ? dispatch_encode<2, true>(pp, k, len, nstripes, st)
-                  : dispatch_encode<2, false>(pp, k, len, nstripes, st);
+            return dispatch_encode<1>(pp, k, len, nstripes, st);
+        return dispatch_encode<2>(pp, k, len, nstripes, st);
     }
     const ArgPtrs pp{*args};
     if (m == 1)
-        return dispatch_encode<1, true>(pp, k, len, 1, st);
-    return dispatch_encode<2, true>(pp, k, len, 1, st);
+        return dispatch_encode<1>(pp, k, len, 1, st);
+    return dispatch_encode<2>(pp, k, len, 1, st);
 }
 
 hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
@@ -517,14 +690,16 @@ hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nst
     const uint32_t f01 = static_cast<uint32_t>(f0) | (static_cast<uint32_t>(f1) << 8);
     if (table) {
         const TablePtrs pp{table, k + m};
+        if (g_variant != 0 && k == 8 && m == 2 && fail_dev)
+            return variant_reconstruct_8p2(g_variant, pp, len, nstripes, fail_dev, st);
         if (m == 1)
-            return dispatch_reconstruct<1, true>(pp, k, len, nstripes, fail_dev, f01, st);
-        return dispatch_reconstruct<2, true>(pp, k, len, nstripes, fail_dev, f01, st);
+            return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, f01, st);
+        return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, f01, st);
     }
     const ArgPtrs pp{*args};
     if (m == 1)
-        return dispatch_reconstruct<1, true>(pp, k, len, 1, fail_dev, f01, st);
-    return dispatch_reconstruct<2, true>(pp, k, len, 1, fail_dev, f01, st);
+        return dispatch_reconstruct<1>(pp, k, len, 1, fail_dev, f01, st);
+    return dispatch_reconstruct<2>(pp, k, len, 1, fail_dev, f01, st);
 }
 
 hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* const* table,
@@ -532,12 +707,12 @@ hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* con
 {
     if (table) {
         const TablePtrs pp{table, k + m};
-        return m == 1 ? go_encode<0, 1, false, true>(pp, k, len, 1, flag, st)
-                      : go_encode<0, 2, false, true>(pp, k, len, 1, flag, st);
+        return m == 1 ? go_encode<0, 1, true, Cfg<256, 2, 0, 0>>(pp, k, len, 1, flag, st)
+                      : go_encode<0, 2, true, Cfg<256, 2, 0, 0>>(pp, k, len, 1, flag, st);
     }
     const ArgPtrs pp{*args};
-    return m == 1 ? go_encode<0, 1, false, true>(pp, k, len, 1, flag, st)
-                  : go_encode<0, 2, false, true>(pp, k, len, 1, flag, st);
+    return m == 1 ? go_encode<0, 1, true, Cfg<256, 2, 0, 0>>(pp, k, len, 1, flag, st)
+                  : go_encode<0, 2, true, Cfg<256, 2, 0, 0>>(pp, k, len, 1, flag, st);
 }
 
 hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,

@@ -1,0 +1,59 @@
+// hbm_probe.hip -- measurement-only kernels (not part of the product library):
+// streaming read / write / copy at 16 B per lane with non-temporal hints, to
+// measure the HBM bandwidth this MI355X actually sustains for each mix.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ src, uint64_t n,
+                                              u32x4* __restrict__ sink)
+{
+    u32x4 acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
+        u32x4 a = __builtin_nontemporal_load(src + i);
+        u32x4 b = i + 256 < n ? __builtin_nontemporal_load(src + i + 256) : 0;
+        u32x4 c = i + 512 < n ? __builtin_nontemporal_load(src + i + 512) : 0;
+        u32x4 d = i + 768 < n ? __builtin_nontemporal_load(src + i + 768) : 0;
+        acc ^= a ^ b ^ c ^ d;
+    }
+    if ((acc.x | acc.y | acc.z | acc.w) == 0x12345678u)  // practically never: keeps the loads live
+        sink[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_write(u32x4* __restrict__ dst, uint64_t n)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        __builtin_nontemporal_store((u32x4)(uint32_t)i, dst + i);
+}
+
+__global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ src,
+                                              u32x4* __restrict__ dst, uint64_t n)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+extern "C" {
+int probe_read(const void* src, uint64_t bytes, void* sink, int grid, void* stream)
+{
+    hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)src, bytes / 16, (u32x4*)sink);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int probe_write(void* dst, uint64_t bytes, int grid, void* stream)
+{
+    hipLaunchKernelGGL(k_write, dim3(grid), dim3(256), 0, (hipStream_t)stream, (u32x4*)dst,
+                       bytes / 16);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int probe_copy(const void* src, void* dst, uint64_t bytes, int grid, void* stream)
+{
+    hipLaunchKernelGGL(k_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)src, (u32x4*)dst, bytes / 16);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""In-process A/B sweep of the RAID6 8+2 kernels: memory layout x kernel variant.
+
+Rounds are interleaved inside one process (cdna_hip_programming.md §5.4 rule 24)
+and the median / min over rounds is reported.  Times come from HIP events on
+the launching stream.
+
+  python tools/sweep.py [--rounds 5] [--iters 10] [--stripes 4096] [--strip-kib 64]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "draid-spdk_amd"))
+sys.path.insert(0, ROOT)
+
+VARIANTS = {0: "default (enc U1, rec U2)", 1: "U2", 2: "512 lanes U1", 3: "128 lanes",
+            4: "chunk-major map", 5: "persistent", 6: "scalar plan", 7: "persist 512 scalar",
+            8: "1024 lanes", 9: "64 lanes", 10: "U1", 11: "512 lanes U2", 12: "U4"}
+
+
+def probe(torch, dev, nbytes, rounds, iters):
+    """Pure read / write / copy ceilings from tools/probe/libprobe.so."""
+    import ctypes as C
+    L = C.CDLL(os.path.join(ROOT, "tools", "probe", "libprobe.so"))
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev).random_(0, 256)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    sink = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = C.c_void_p(stream.cuda_stream)
+    out = []
+    for grid in (2048, 4096, 8192, 16384):
+        ops = {"read": (lambda: L.probe_read(C.c_void_p(a.data_ptr()), C.c_uint64(nbytes),
+                                             C.c_void_p(sink.data_ptr()), grid, sh), nbytes),
+               "write": (lambda: L.probe_write(C.c_void_p(b.data_ptr()), C.c_uint64(nbytes), grid,
+                                               sh), nbytes),
+               "copy": (lambda: L.probe_copy(C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()),
+                                             C.c_uint64(nbytes), grid, sh), 2 * nbytes)}
+        for name, (fn, moved) in ops.items():
+            ts = []
+            for _ in range(rounds):
+                fn()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(iters):
+                    fn()
+                e1.record(stream)
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3 / iters)
+            med = float(np.median(ts))
+            out.append({"probe": name, "grid": grid, "median_us": round(med, 2),
+                        "gb_s": round(moved / (med * 1e-6) / 1e9, 1)})
+            print(f"probe {name:5s} grid {grid:6d} {med:9.2f} us {out[-1]['gb_s']:8.1f} GB/s")
+    del a, b
+    return out
+
+
+def make_layout(torch, name, k, m, S, B, dev):
+    n = k + m
+    if name.startswith("stripe_major"):
+        gap = int(name.split("gap")[1]) if "gap" in name else 0
+        ss = S + gap
+        buf = torch.empty(B * n * ss, dtype=torch.uint8, device=dev)
+        idx = torch.arange(B * n, dtype=torch.int64, device=dev)
+        table = buf.data_ptr() + idx * ss
+    elif name == "strip_major":
+        buf = torch.empty(n * B * S, dtype=torch.uint8, device=dev)
+        s = torch.arange(B, dtype=torch.int64, device=dev).repeat_interleave(n)
+        j = torch.arange(n, dtype=torch.int64, device=dev).repeat(B)
+        table = buf.data_ptr() + j * (B * S) + s * S
+    else:
+        raise ValueError(name)
+    buf.random_(0, 256)
+    return buf, table.contiguous()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--strip-kib", type=int, default=64)
+    ap.add_argument("--layouts", default="stripe_major,stripe_major_gap256,stripe_major_gap4096,strip_major")
+    ap.add_argument("--variants", default="0,1,2,8,10,11,12")
+    ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
+    args = ap.parse_args()
+
+    import torch
+    import draid_ec as ec
+    import bench
+
+    dev = torch.device("cuda", 0)
+    k, m, S, B = 8, 2, args.strip_kib * 1024, args.stripes
+    probes = probe(torch, dev, (k + m) * S * B, args.rounds, args.iters) if args.probe else []
+    fail = torch.from_numpy(bench.failure_pairs(B, k, 0x1234).reshape(-1)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    layouts = {}
+    for name in args.layouts.split(","):
+        buf, table = make_layout(torch, name, k, m, S, B, dev)
+        layouts[name] = (buf, table, ec.make_batch(k, m, S, B, table))
+    variants = [int(v) for v in args.variants.split(",")]
+    res = {f"{l}|{v}|{op}": [] for l in layouts for v in variants for op in ("enc", "rec")}
+    nbytes = (k + m) * S * B
+    for r in range(args.rounds):
+        for lname, (_, _, batch) in layouts.items():
+            for v in variants:
+                ec.set_variant(v)
+                for op in ("enc", "rec"):
+                    fn = (lambda: ec.encode(batch, sh)) if op == "enc" else \
+                         (lambda: ec.reconstruct(batch, fail, sh))
+                    fn()
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(args.iters):
+                        fn()
+                    e1.record(stream)
+                    e1.synchronize()
+                    us = e0.elapsed_time(e1) * 1e3 / args.iters
+                    res[f"{lname}|{v}|{op}"].append(us)
+    ec.set_variant(0)
+    summary = []
+    for key, vals in res.items():
+        lname, v, op = key.split("|")
+        med = float(np.median(vals))
+        summary.append({"layout": lname, "variant": int(v), "desc": VARIANTS[int(v)], "op": op,
+                        "median_us": round(med, 2), "min_us": round(min(vals), 2),
+                        "hbm_gb_s": round(nbytes / (med * 1e-6) / 1e9, 1)})
+    summary.sort(key=lambda d: (d["op"], d["median_us"]))
+    for d in summary:
+        print(f'{d["op"]} {d["layout"]:24s} v{d["variant"]} {d["desc"]:22s} '
+              f'{d["median_us"]:9.2f} us  {d["hbm_gb_s"]:8.1f} GB/s')
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump({"config": vars(args), "results": summary, "probes": probes}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
