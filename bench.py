@@ -41,6 +41,19 @@ def shard_range(nstripes_total: int, rank: int, world: int) -> tuple[int, int]:
     return nstripes_total * rank // world, nstripes_total * (rank + 1) // world
 
 
+def reduce_timing(elapsed: float, units: float, device) -> tuple[float, float]:
+    """Contract aggregation across ranks: max of the wall times, sum of the units."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed, units
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    u = torch.tensor([units], dtype=torch.float64, device=device)
+    dist.all_reduce(u, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(u.item())
+
+
 def failure_pairs(nstripes: int, k: int, seed: int) -> np.ndarray:
     """[nstripes, 2] distinct lost data indices per stripe (dual data failure)."""
     rng = np.random.default_rng(seed)
@@ -154,13 +167,7 @@ def main() -> None:
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     rec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     units = 2.0 * k * S * B * args.steps  # user-data bytes through both passes
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        u = torch.tensor([units], dtype=torch.float64, device=dev)
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
-        units = float(u.item())
+    elapsed, units = reduce_timing(elapsed, units, dev)
 
     verified = None
     if not args.no_verify:
