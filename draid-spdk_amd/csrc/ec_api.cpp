@@ -20,9 +20,10 @@ using draid::ArgPtrTable;
 using draid::kMaxArgPtrs;
 
 namespace {
-
 thread_local char t_err[256] = "";
+}  // namespace
 
+namespace draid {
 int fail_hip(hipError_t e, const char* what)
 {
     snprintf(t_err, sizeof(t_err), "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
@@ -34,6 +35,12 @@ int fail_arg(const char* what)
     snprintf(t_err, sizeof(t_err), "invalid argument: %s", what);
     return 1;
 }
+}  // namespace draid
+
+using draid::fail_arg;
+using draid::fail_hip;
+
+namespace {
 
 hipStream_t sync_stream() { return hipStreamPerThread; }
 

@@ -488,6 +488,57 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
     }
 }
 
+// ------------------------------------------------------------ segment work lists
+
+// Scatter-gather form (ec_ctx.cpp): a batch of variable-length segments, each
+// one contiguous run across the k+m strips of a stripe (what raid5_xor_stripe,
+// raid5_simple.c:141-203, hands to one xor_gen call).  The host expands the
+// segments into work items (segment, chunk) so one launch covers them all.
+struct WorkItem {
+    uint32_t seg;
+    uint32_t chunk;
+};
+
+template <int KT, int M, bool CHECK, class C>
+__global__ __launch_bounds__(C::NTHR) void k_encode_work(TablePtrs pp, uint32_t k_rt,
+                                                         const uint32_t* seg_len,
+                                                         const WorkItem* work, uint32_t nwork)
+{
+    constexpr uint64_t CB = static_cast<uint64_t>(C::NTHR) * C::U * 16;
+    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
+    for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
+        const WorkItem w = work[b];
+        const uint32_t len = seg_len[w.seg];
+        const uint32_t cps = static_cast<uint32_t>((len + CB - 1) / CB);
+        encode_item<KT, M, CHECK, C>(pp, w.seg, w.chunk, k, len, cps);
+    }
+}
+
+template <int KT, int M, class C>
+__global__ __launch_bounds__(C::NTHR) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
+                                                              const uint32_t* seg_len,
+                                                              const uint8_t* fail,
+                                                              const WorkItem* work,
+                                                              uint32_t nwork)
+{
+    __shared__ LdsGf lds;
+    const uint8_t* l_exp = reinterpret_cast<const uint8_t*>(lds.w);
+    const uint8_t* l_log = l_exp + 512;
+    constexpr uint64_t CB = static_cast<uint64_t>(C::NTHR) * C::U * 16;
+    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
+    stage_gf_tables<C::NTHR>(lds);
+    for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
+        const WorkItem w = work[b];
+        const uint32_t len = seg_len[w.seg];
+        const uint32_t cps = static_cast<uint32_t>((len + CB - 1) / CB);
+        RecPlan pl = decode_failures<M>(k, fail[2 * (size_t)w.seg], fail[2 * (size_t)w.seg + 1]);
+        if (pl.skip)
+            continue;
+        reconstruct_item<KT, M, C>(pp, w.seg, w.chunk, k, len, cps, pl,
+                                   [&](RecPlan& p) { plan_constants(p, l_exp, l_log); });
+    }
+}
+
 // ------------------------------------------------------------ gf_vect_mul
 
 __global__ __launch_bounds__(kThreads) void k_gf_vect_mul(const uint8_t* src, uint8_t* dst,
@@ -713,6 +764,88 @@ hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* con
     const ArgPtrs pp{*args};
     return m == 1 ? go_encode<0, 1, true, Cfg<256, 2, 0, 0>>(pp, k, len, 1, flag, st)
                   : go_encode<0, 2, true, Cfg<256, 2, 0, 0>>(pp, k, len, 1, flag, st);
+}
+
+// ---- segment work lists
+
+template <int KT, int M, class C>
+static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, const uint32_t* seg_len,
+                                 const void* work, uint32_t nwork, hipStream_t st)
+{
+    if (nwork == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                       TablePtrs{tab, k + M}, k, seg_len, static_cast<const WorkItem*>(work),
+                       nwork);
+    return hipGetLastError();
+}
+
+template <int KT, int M, class C>
+static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t k,
+                                      const uint32_t* seg_len, const uint8_t* fail,
+                                      const void* work, uint32_t nwork, hipStream_t st)
+{
+    if (nwork == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                       TablePtrs{tab, k + M}, k, seg_len, fail,
+                       static_cast<const WorkItem*>(work), nwork);
+    return hipGetLastError();
+}
+
+uint32_t work_chunk_bytes(int op, uint32_t k)
+{
+    int u = 2;
+    switch (k) {
+#define DRAID_CASE(K)                                       \
+    case K:                                                 \
+        u = op == 0 ? enc_unroll(K) : rec_unroll(K); \
+        break;
+        DRAID_FOR_EACH_K(DRAID_CASE)
+#undef DRAID_CASE
+    default:
+        break;
+    }
+    return 256u * static_cast<uint32_t>(u) * 16u;
+}
+
+hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,
+                              const uint32_t* seg_len, const void* work, uint32_t nwork,
+                              hipStream_t st)
+{
+    switch (k) {
+#define DRAID_CASE(K)                                                                          \
+    case K:                                                                                    \
+        return m == 1 ? go_encode_work<K, 1, CfgDefault<enc_unroll(K)>>(table, k, seg_len, work, \
+                                                                        nwork, st)            \
+                      : go_encode_work<K, 2, CfgDefault<enc_unroll(K)>>(table, k, seg_len, work, \
+                                                                        nwork, st);
+        DRAID_FOR_EACH_K(DRAID_CASE)
+#undef DRAID_CASE
+    default:
+        return m == 1 ? go_encode_work<0, 1, CfgDefault<2>>(table, k, seg_len, work, nwork, st)
+                      : go_encode_work<0, 2, CfgDefault<2>>(table, k, seg_len, work, nwork, st);
+    }
+}
+
+hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
+                                   const uint32_t* seg_len, const uint8_t* fail, const void* work,
+                                   uint32_t nwork, hipStream_t st)
+{
+    switch (k) {
+#define DRAID_CASE(K)                                                                         \
+    case K:                                                                                   \
+        return m == 1 ? go_reconstruct_work<K, 1, CfgDefault<rec_unroll(K)>>(                 \
+                            table, k, seg_len, fail, work, nwork, st)                        \
+                      : go_reconstruct_work<K, 2, CfgDefault<rec_unroll(K)>>(                 \
+                            table, k, seg_len, fail, work, nwork, st);
+        DRAID_FOR_EACH_K(DRAID_CASE)
+#undef DRAID_CASE
+    default:
+        return m == 1
+                   ? go_reconstruct_work<0, 1, CfgDefault<2>>(table, k, seg_len, fail, work, nwork, st)
+                   : go_reconstruct_work<0, 2, CfgDefault<2>>(table, k, seg_len, fail, work, nwork, st);
+    }
 }
 
 hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,

@@ -38,6 +38,21 @@ hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len,
 hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,
                               uint8_t* dst, hipStream_t stream);
 
+// Segment work lists (scatter-gather, ec_ctx.cpp).  op: 0 encode, 1 reconstruct.
+// A work item is {segment, chunk}; chunk covers work_chunk_bytes(op, k) bytes.
+uint32_t work_chunk_bytes(int op, uint32_t k);
+hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,
+                              const uint32_t* seg_len, const void* work, uint32_t nwork,
+                              hipStream_t stream);
+hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
+                                   const uint32_t* seg_len, const uint8_t* fail, const void* work,
+                                   uint32_t nwork, hipStream_t stream);
+
+// Error reporting shared by every C entry point (ec_api.cpp): records the
+// message for draid_ec_last_error(); fail_hip returns -hipError, fail_arg 1.
+int fail_hip(hipError_t e, const char* what);
+int fail_arg(const char* what);
+
 // Variant selector for A/B experiments inside one process (0 = default).
 void set_variant(int v);
 int get_variant();

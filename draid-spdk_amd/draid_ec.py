@@ -26,8 +26,15 @@ EXPORTS = (
     "draid_ec_device_count", "draid_ec_stream_create", "draid_ec_stream_destroy",
     "draid_ec_stream_query", "draid_ec_stream_synchronize", "draid_ec_device_alloc",
     "draid_ec_device_free", "draid_ec_host_register", "draid_ec_host_unregister",
-    "draid_ec_memcpy_async",
+    "draid_ec_memcpy_async", "draid_ec_ctx_create", "draid_ec_ctx_destroy",
+    "draid_ec_ctx_stream", "draid_ec_ctx_encode_sg", "draid_ec_ctx_reconstruct_sg",
+    "draid_ec_ctx_flush", "draid_ec_ctx_query", "draid_ec_ctx_synchronize",
+    "draid_ec_ctx_queued",
 )
+
+
+class IoVec(C.Structure):
+    _fields_ = [("iov_base", C.c_void_p), ("iov_len", C.c_size_t)]
 
 
 class StripeBatch(C.Structure):
@@ -86,6 +93,17 @@ def lib() -> C.CDLL:
         L.draid_ec_host_register.argtypes = [vp, C.c_size_t]
         L.draid_ec_memcpy_async.argtypes = [vp, vp, C.c_size_t, i32, vp]
         L.draid_ec_set_variant.argtypes = [i32]
+        L.draid_ec_ctx_create.argtypes = [C.POINTER(vp)]
+        for f in ("draid_ec_ctx_destroy", "draid_ec_ctx_flush", "draid_ec_ctx_query",
+                  "draid_ec_ctx_synchronize"):
+            getattr(L, f).argtypes = [vp]
+        L.draid_ec_ctx_stream.argtypes = [vp]
+        L.draid_ec_ctx_stream.restype = vp
+        L.draid_ec_ctx_queued.argtypes = [vp]
+        L.draid_ec_ctx_queued.restype = C.c_uint64
+        L.draid_ec_ctx_encode_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t]
+        L.draid_ec_ctx_reconstruct_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp,
+                                                  C.c_size_t, i32, vp]
         _lib = L
     return _lib
 
@@ -181,6 +199,61 @@ def stream_query(stream: int) -> int:
 
 def stream_synchronize(stream: int) -> None:
     _check(lib().draid_ec_stream_synchronize(stream), "stream_synchronize")
+
+
+# ---- scatter-gather context ----
+
+class Ctx:
+    """Owns a draid_ec_ctx (one stream + descriptor ring); single-threaded."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        _check(lib().draid_ec_ctx_create(C.byref(h)), "ctx_create")
+        self.h = h.value
+
+    def close(self):
+        if self.h:
+            lib().draid_ec_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _lists(strips):
+        """strips: list (k+m) of lists of (ptr, len) runs."""
+        arrs = [(IoVec * max(1, len(s)))(*[IoVec(_ptr(p), n) for p, n in s]) for s in strips]
+        heads = (C.c_void_p * len(strips))(*[C.addressof(a) for a in arrs])
+        cnts = (C.c_int * len(strips))(*[len(s) for s in strips])
+        return arrs, heads, cnts
+
+    def encode_sg(self, k, m, strips, length, offsets=None):
+        arrs, heads, cnts = self._lists(strips)
+        off = (C.c_size_t * len(strips))(*offsets) if offsets else None
+        return _check(lib().draid_ec_ctx_encode_sg(self.h, k, m, heads, cnts, off, length),
+                      "ctx_encode_sg")
+
+    def reconstruct_sg(self, k, m, strips, length, fail, offsets=None):
+        arrs, heads, cnts = self._lists(strips)
+        off = (C.c_size_t * len(strips))(*offsets) if offsets else None
+        f = (C.c_int * max(1, len(fail)))(*fail)
+        return _check(lib().draid_ec_ctx_reconstruct_sg(self.h, k, m, heads, cnts, off, length,
+                                                        len(fail), f), "ctx_reconstruct_sg")
+
+    def flush(self):
+        return _check(lib().draid_ec_ctx_flush(self.h), "ctx_flush")
+
+    def query(self):
+        return _check(lib().draid_ec_ctx_query(self.h), "ctx_query")
+
+    def synchronize(self):
+        return _check(lib().draid_ec_ctx_synchronize(self.h), "ctx_synchronize")
+
+    def queued(self):
+        return lib().draid_ec_ctx_queued(self.h)
 
 
 def set_variant(v: int) -> None:

@@ -31,6 +31,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <sys/uio.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -110,6 +111,42 @@ int draid_ec_encode(const draid_ec_stripe_batch *batch, void *stream);
  * ignored; a stripe with more failures than m is left untouched. */
 int draid_ec_reconstruct(const draid_ec_stripe_batch *batch, const uint8_t *fail,
                          void *stream);
+
+/* ------------------------------------------------------------------------
+ * 2b. Scatter-gather stripes through a per-channel context
+ *
+ * The reference walks each chunk's iovec list and calls isa-l once per
+ * contiguous run (raid5_xor_iovs, raid5.c:221-283; raid5_xor_stripe,
+ * raid5_simple.c:141-203).  A context runs the same walk on the host but queues
+ * each run as a gather descriptor; draid_ec_ctx_flush() uploads all queued
+ * descriptors with one DMA and launches one kernel per (op, k, m) group.
+ * A context owns a stream and is used by one thread (one per SPDK io_channel).
+ * ---------------------------------------------------------------------- */
+
+typedef struct draid_ec_ctx draid_ec_ctx;
+
+int draid_ec_ctx_create(draid_ec_ctx **ctx);       /* on the current device */
+int draid_ec_ctx_destroy(draid_ec_ctx *ctx);
+void *draid_ec_ctx_stream(draid_ec_ctx *ctx);
+
+/* Queue one stripe's encode.  Strip j (k data, then P, then Q) is `len` bytes
+ * starting `offset[j]` bytes into iovs[j][0 .. iovcnt[j]) (offset may be NULL).
+ * Every iov_base must be device-accessible. */
+int draid_ec_ctx_encode_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m,
+                           const struct iovec *const *iovs, const int *iovcnt,
+                           const size_t *offset, size_t len);
+
+/* Queue one stripe's reconstruct of the nfail (<= m) strips listed in fail[]. */
+int draid_ec_ctx_reconstruct_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m,
+                                const struct iovec *const *iovs, const int *iovcnt,
+                                const size_t *offset, size_t len, int nfail, const int *fail);
+
+/* Launch everything queued (non-blocking; blocks only if the descriptor ring
+ * is 4 flushes behind).  draid_ec_ctx_query: 0 idle, 1 running, < 0 error. */
+int draid_ec_ctx_flush(draid_ec_ctx *ctx);
+int draid_ec_ctx_query(draid_ec_ctx *ctx);
+int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);
+uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last flush */
 
 /* ------------------------------------------------------------------------
  * 3. Runtime helpers (device, streams, memory)
