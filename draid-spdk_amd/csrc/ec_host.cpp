@@ -1,0 +1,237 @@
+// ec_host.cpp -- host-resident stripes (SPDK bdev buffers in pinned host memory).
+//
+// The reference computes parity in place in host buffers: spdk_dma_malloc'd
+// stripe buffers and user iovecs (raid5.c:1326-1359, 743-777).  For host
+// stripes the GPU path is: copy the k data strips in (hipMemcpy2DAsync, one per
+// strip index per chunk of stripes), encode in HBM, copy P (and Q) back out.
+// Chunks rotate over kStreams streams, each with its own device staging area,
+// so copy-in of one chunk, the kernel of another and copy-out of a third run
+// concurrently (separate SDMA engines for H2D and D2H).  Stream order alone
+// protects each staging area: its next chunk's copy-in is queued behind its
+// previous chunk's copy-out.  The calls are synchronous.
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/draid_ec.h"
+#include "ec_launch.hpp"
+
+namespace {
+
+constexpr int kStreams = 3;
+
+struct Stage {
+    hipStream_t stream = nullptr;
+    uint8_t* dev = nullptr;       // [chunk][k+m][S]
+    size_t dev_bytes = 0;
+    void** table = nullptr;       // device pointer table for the staged chunk
+    uint8_t* fail = nullptr;      // device [chunk][2]
+    size_t table_entries = 0;
+    uint32_t k = 0, m = 0, chunk = 0;
+    uint64_t S = 0;
+};
+
+struct HostEngine {
+    int device = -1;
+    Stage st[kStreams];
+    ~HostEngine() { reset(); }
+    void reset()
+    {
+        for (Stage& s : st) {
+            if (s.stream)
+                (void)hipStreamSynchronize(s.stream);
+            if (s.dev)
+                (void)hipFree(s.dev);
+            if (s.table)
+                (void)hipFree(s.table);
+            if (s.fail)
+                (void)hipFree(s.fail);
+            if (s.stream)
+                (void)hipStreamDestroy(s.stream);
+            s = Stage();
+        }
+    }
+};
+
+thread_local HostEngine t_eng;
+
+int prepare(Stage& s, uint32_t k, uint32_t m, uint64_t S, uint32_t chunk)
+{
+    hipError_t e;
+    if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
+        return draid::fail_hip(e, "hipStreamCreate(host engine)");
+    if (s.k == k && s.m == m && s.S == S && s.chunk == chunk)
+        return 0;
+    (void)hipStreamSynchronize(s.stream);
+    const size_t bytes = static_cast<size_t>(chunk) * (k + m) * S;
+    if (s.dev_bytes < bytes) {
+        if (s.dev)
+            (void)hipFree(s.dev);
+        s.dev = nullptr;
+        s.dev_bytes = 0;
+        if ((e = hipMalloc(&s.dev, bytes)) != hipSuccess)
+            return draid::fail_hip(e, "hipMalloc(host staging)");
+        s.dev_bytes = bytes;
+    }
+    const size_t entries = static_cast<size_t>(chunk) * (k + m);
+    if (s.table_entries < entries) {
+        if (s.table)
+            (void)hipFree(s.table);
+        if (s.fail)
+            (void)hipFree(s.fail);
+        s.table = nullptr;
+        s.fail = nullptr;
+        s.table_entries = 0;
+        if ((e = hipMalloc(&s.table, entries * sizeof(void*))) != hipSuccess)
+            return draid::fail_hip(e, "hipMalloc(host staging table)");
+        if ((e = hipMalloc(&s.fail, static_cast<size_t>(chunk) * 2)) != hipSuccess)
+            return draid::fail_hip(e, "hipMalloc(host staging fail)");
+        s.table_entries = entries;
+    }
+    std::vector<void*> t(entries);
+    for (size_t i = 0; i < entries; ++i)
+        t[i] = s.dev + i * S;  // stripe-major: stripe c strip j at (c*(k+m)+j)*S
+    if ((e = hipMemcpy(s.table, t.data(), entries * sizeof(void*), hipMemcpyHostToDevice)) !=
+        hipSuccess)
+        return draid::fail_hip(e, "hipMemcpy(host staging table)");
+    s.k = k;
+    s.m = m;
+    s.S = S;
+    s.chunk = chunk;
+    return 0;
+}
+
+int check_host(const draid_ec_host_stripes* h)
+{
+    if (!h || !h->base)
+        return draid::fail_arg("host stripes descriptor / base is NULL");
+    if (h->k < 1 || h->k > 255 || h->m < 1 || h->m > 2 || h->flags != 0)
+        return draid::fail_arg("host stripes need 1 <= k <= 255, m in {1,2}, flags == 0");
+    if (h->strip_stride < h->strip_len)
+        return draid::fail_arg("strip_stride < strip_len");
+    return 0;
+}
+
+// Shared driver: per chunk, copy in `in_lo..in_hi` strip indices, run `launch`,
+// copy out per `copy_out`.
+template <class Launch, class CopyOut>
+int run_chunks(const draid_ec_host_stripes* h, uint32_t chunk, uint32_t in_lo, uint32_t in_hi,
+               Launch&& launch, CopyOut&& copy_out)
+{
+    const uint32_t k = h->k, m = h->m, n = k + m;
+    const uint64_t S = h->strip_len;
+    if (chunk == 0)
+        chunk = 64;
+    chunk = std::min(chunk, std::max<uint32_t>(1, h->nstripes));
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (t_eng.device != dev) {
+        t_eng.reset();
+        t_eng.device = dev;
+    }
+    for (Stage& s : t_eng.st) {
+        int rc = prepare(s, k, m, S, chunk);
+        if (rc)
+            return rc;
+    }
+    uint8_t* base = static_cast<uint8_t*>(h->base);
+    hipError_t e = hipSuccess;
+    for (uint32_t c0 = 0, ci = 0; c0 < h->nstripes; c0 += chunk, ++ci) {
+        Stage& s = t_eng.st[ci % kStreams];
+        const uint32_t rows = std::min(chunk, h->nstripes - c0);
+        uint8_t* hb = base + static_cast<uint64_t>(c0) * h->stripe_stride;
+        for (uint32_t j = in_lo; j < in_hi; ++j) {
+            e = hipMemcpy2DAsync(s.dev + j * S, n * S, hb + j * h->strip_stride, h->stripe_stride,
+                                 S, rows, hipMemcpyHostToDevice, s.stream);
+            if (e != hipSuccess)
+                return draid::fail_hip(e, "hipMemcpy2DAsync(H2D strips)");
+        }
+        if ((e = launch(s, c0, rows)) != hipSuccess)
+            return draid::fail_hip(e, "launch (host path)");
+        if ((e = copy_out(s, c0, rows, hb)) != hipSuccess)
+            return draid::fail_hip(e, "copy-out (host path)");
+    }
+    for (Stage& s : t_eng.st)
+        if ((e = hipStreamSynchronize(s.stream)) != hipSuccess)
+            return draid::fail_hip(e, "hipStreamSynchronize(host path)");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int draid_ec_host_encode(const draid_ec_host_stripes* h, uint32_t chunk_stripes)
+{
+    int rc = check_host(h);
+    if (rc || h->nstripes == 0 || h->strip_len == 0)
+        return rc;
+    const uint32_t k = h->k, m = h->m, n = k + m;
+    const uint64_t S = h->strip_len;
+    return run_chunks(
+        h, chunk_stripes, 0, k,
+        [&](Stage& s, uint32_t, uint32_t rows) {
+            return draid::launch_encode(k, m, S, rows,
+                                        reinterpret_cast<const uint8_t* const*>(s.table), nullptr,
+                                        s.stream);
+        },
+        [&](Stage& s, uint32_t, uint32_t rows, uint8_t* hb) {
+            for (uint32_t j = k; j < n; ++j) {
+                hipError_t e =
+                    hipMemcpy2DAsync(hb + j * h->strip_stride, h->stripe_stride, s.dev + j * S,
+                                     n * S, S, rows, hipMemcpyDeviceToHost, s.stream);
+                if (e != hipSuccess)
+                    return e;
+            }
+            return hipSuccess;
+        });
+}
+
+int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fail,
+                              uint32_t chunk_stripes)
+{
+    int rc = check_host(h);
+    if (rc || h->nstripes == 0 || h->strip_len == 0)
+        return rc;
+    if (!fail)
+        return draid::fail_arg("host reconstruct: fail table is NULL");
+    const uint32_t k = h->k, m = h->m, n = k + m;
+    const uint64_t S = h->strip_len;
+    return run_chunks(
+        h, chunk_stripes, 0, n,
+        [&](Stage& s, uint32_t c0, uint32_t rows) {
+            hipError_t e = hipMemcpyAsync(s.fail, fail + 2 * static_cast<size_t>(c0), 2 * rows,
+                                          hipMemcpyHostToDevice, s.stream);
+            if (e != hipSuccess)
+                return e;
+            return draid::launch_reconstruct(k, m, S, rows,
+                                             reinterpret_cast<const uint8_t* const*>(s.table),
+                                             nullptr, s.fail, 0xff, 0xff, s.stream);
+        },
+        [&](Stage& s, uint32_t c0, uint32_t rows, uint8_t* hb) {
+            for (uint32_t r = 0; r < rows; ++r) {
+                // the strips the kernel regenerated (same decoding as decode_failures)
+                const uint8_t* f = fail + 2 * static_cast<size_t>(c0 + r);
+                const bool v0 = f[0] < n;
+                const bool v1 = f[1] < n && !(v0 && f[1] == f[0]);
+                if ((v0 ? 1u : 0u) + (v1 ? 1u : 0u) > m)
+                    continue;  // unrecoverable: the kernel left it untouched
+                for (int t = 0; t < 2; ++t) {
+                    const uint32_t j = f[t];
+                    if (!(t == 0 ? v0 : v1))
+                        continue;
+                    hipError_t e = hipMemcpyAsync(hb + r * h->stripe_stride + j * h->strip_stride,
+                                                  s.dev + (static_cast<uint64_t>(r) * n + j) * S,
+                                                  S, hipMemcpyDeviceToHost, s.stream);
+                    if (e != hipSuccess)
+                        return e;
+                }
+            }
+            return hipSuccess;
+        });
+}
+
+}  // extern "C"

@@ -29,8 +29,14 @@ EXPORTS = (
     "draid_ec_memcpy_async", "draid_ec_ctx_create", "draid_ec_ctx_destroy",
     "draid_ec_ctx_stream", "draid_ec_ctx_encode_sg", "draid_ec_ctx_reconstruct_sg",
     "draid_ec_ctx_flush", "draid_ec_ctx_query", "draid_ec_ctx_synchronize",
-    "draid_ec_ctx_queued",
+    "draid_ec_ctx_queued", "draid_ec_host_encode", "draid_ec_host_reconstruct",
 )
+
+
+class HostStripes(C.Structure):
+    _fields_ = [("k", C.c_uint32), ("m", C.c_uint32), ("strip_len", C.c_uint64),
+                ("nstripes", C.c_uint32), ("flags", C.c_uint32), ("base", C.c_void_p),
+                ("strip_stride", C.c_uint64), ("stripe_stride", C.c_uint64)]
 
 
 class IoVec(C.Structure):
@@ -104,6 +110,8 @@ def lib() -> C.CDLL:
         L.draid_ec_ctx_encode_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t]
         L.draid_ec_ctx_reconstruct_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp,
                                                   C.c_size_t, i32, vp]
+        L.draid_ec_host_encode.argtypes = [C.POINTER(HostStripes), C.c_uint32]
+        L.draid_ec_host_reconstruct.argtypes = [C.POINTER(HostStripes), vp, C.c_uint32]
         _lib = L
     return _lib
 
@@ -199,6 +207,20 @@ def stream_query(stream: int) -> int:
 
 def stream_synchronize(stream: int) -> None:
     _check(lib().draid_ec_stream_synchronize(stream), "stream_synchronize")
+
+
+# ---- host-resident stripes ----
+
+def host_encode(base, k, m, strip_len, nstripes, strip_stride, stripe_stride, chunk=0) -> int:
+    h = HostStripes(k, m, strip_len, nstripes, 0, _ptr(base), strip_stride, stripe_stride)
+    return _check(lib().draid_ec_host_encode(C.byref(h), chunk), "host_encode")
+
+
+def host_reconstruct(base, k, m, strip_len, nstripes, strip_stride, stripe_stride, fail,
+                     chunk=0) -> int:
+    h = HostStripes(k, m, strip_len, nstripes, 0, _ptr(base), strip_stride, stripe_stride)
+    return _check(lib().draid_ec_host_reconstruct(C.byref(h), _ptr(fail), chunk),
+                  "host_reconstruct")
 
 
 # ---- scatter-gather context ----

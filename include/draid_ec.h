@@ -149,6 +149,34 @@ int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);
 uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last flush */
 
 /* ------------------------------------------------------------------------
+ * 2c. Host-resident stripes (PCIe-inclusive path)
+ *
+ * SPDK's stripe buffers are host hugepages.  These calls copy the input strips
+ * in (hipMemcpy2DAsync per strip index over a chunk of stripes), run the kernel
+ * in HBM and copy the results back, pipelined over three streams.  Register or
+ * pin the host range first (draid_ec_host_register) for full PCIe speed.
+ * Synchronous.  chunk_stripes = stripes per pipeline stage (0 = 64).
+ * ---------------------------------------------------------------------- */
+
+typedef struct draid_ec_host_stripes {
+    uint32_t k, m;           /* as draid_ec_stripe_batch                          */
+    uint64_t strip_len;      /* bytes per strip                                   */
+    uint32_t nstripes;
+    uint32_t flags;          /* reserved, must be 0                               */
+    void *base;              /* HOST: strip j of stripe s at                      */
+    uint64_t strip_stride;   /*   base + s*stripe_stride + j*strip_stride         */
+    uint64_t stripe_stride;
+} draid_ec_host_stripes;
+
+/* Data strips in, P (and Q) out. */
+int draid_ec_host_encode(const draid_ec_host_stripes *h, uint32_t chunk_stripes);
+
+/* All k+m strips in, the failed strips (HOST fail[nstripes][2], as
+ * draid_ec_reconstruct) out. */
+int draid_ec_host_reconstruct(const draid_ec_host_stripes *h, const uint8_t *fail,
+                              uint32_t chunk_stripes);
+
+/* ------------------------------------------------------------------------
  * 3. Runtime helpers (device, streams, memory)
  * ---------------------------------------------------------------------- */
 
