@@ -62,24 +62,60 @@ def failure_pairs(nstripes: int, k: int, seed: int) -> np.ndarray:
     return np.stack([x, y], axis=1).astype(np.uint8)
 
 
-def load_pmc_traffic(workload: str):
-    """HBM bytes per encode launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_<workload>.json, written by tools/collect_pmc.py), or None."""
+def failure_single(nstripes: int, k: int, seed: int) -> np.ndarray:
+    """[nstripes, 2] one lost data index per stripe (x = splitmix-style draw mod k)."""
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, k, nstripes)
+    return np.stack([x, np.full(nstripes, 0xFF)], axis=1).astype(np.uint8)
+
+
+# BASELINE.json configs the harness can run.  The default (no --config) is the
+# headline metric's workload; the others are measured with the same harness and
+# recorded in DESIGN.md (they are not the driver's bench line).
+CONFIGS = {
+    # configs[2] -- the metric's workload: RAID6 8+2 encode + reconstruct at 64 KiB
+    "raid6_8p2_64k": dict(k=8, m=2, strip_kib=64, stripes=4096, failures="dual",
+                          label="RAID6 8+2 P+Q encode + dual-data-failure reconstruct, 64 KiB "
+                                "strips (configs[2])"),
+    # configs[1] -- RAID5 4+1 XOR encode (+ single-failure reconstruct), 64 KiB
+    "raid5_4p1_64k": dict(k=4, m=1, strip_kib=64, stripes=4096, failures="single",
+                          label="RAID5 4+1 XOR encode + single-failure reconstruct, 64 KiB "
+                                "strips (configs[1])"),
+    # configs[3] -- RAID6 8+2 single-failure degraded read, 128 KiB
+    "raid6_8p2_128k_single": dict(k=8, m=2, strip_kib=128, stripes=4096, failures="single",
+                                  label="RAID6 8+2 encode + single-failure reconstruct, 128 KiB "
+                                        "strips (configs[3])"),
+    # configs[4] -- RAID6 16+2 dual failure, 256 KiB; 4096 stripes over 8 GPUs = 512 per GPU
+    "raid6_16p2_256k_dual": dict(k=16, m=2, strip_kib=256, stripes=512, failures="dual",
+                                 label="RAID6 16+2 encode + dual-data-failure reconstruct, 256 KiB "
+                                       "strips (configs[4])"),
+}
+
+
+def reconstruct_bytes_per_stripe(k: int, m: int, S: int, failures: str) -> int:
+    """Algorithmic HBM bytes of one stripe's reconstruct."""
+    if failures == "dual":
+        return (k + 2) * S          # k-2 data + P + Q read, 2 written
+    return (k + 1) * S              # k-1 data + P read, 1 written
+
+
+def load_pmc(workload: str):
+    """Per-launch HBM bytes of each kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_<workload>.json, tools/collect_pmc.py), or None."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
-        d = json.load(f)
-    return d.get("encode_hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+        return json.load(f), os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(k: int, m: int, S: int, seconds: float, threads: int) -> dict:
+def cpu_baseline(k: int, m: int, S: int, failures: str, seconds: float, threads: int) -> dict:
     """The C oracle (isa-l v2.30 restatement, oracle/) timed on the host cores on
-    a bounded sample of the same workload: 64 stripes, encode + dual reconstruct."""
+    a bounded sample of the same workload: 64 stripes, encode + reconstruct."""
     import oracle
     B = 64
     buf = np.frombuffer(np.random.default_rng(1).bytes((k + m) * S * B), np.uint8).copy()
-    fail = failure_pairs(B, k, 7).reshape(-1)
+    fail = (failure_pairs if failures == "dual" else failure_single)(B, k, 7).reshape(-1)
     el, passes = oracle.bench_encode_reconstruct(buf, k, m, S, B, S, (k + m) * S, fail, True,
                                                  threads, seconds)
     if el <= 0:
@@ -87,7 +123,7 @@ def cpu_baseline(k: int, m: int, S: int, seconds: float, threads: int) -> dict:
     user = 2.0 * k * S * B * passes
     return {"value": round(user / el / GIB, 3), "unit": "GiB/s", "cores": threads,
             "kind": "port",
-            "sample": f"{B} stripes x RAID6 {k}+{m} x {S // 1024} KiB, encode + dual-data "
+            "sample": f"{B} stripes x {k}+{m} x {S // 1024} KiB, encode + {failures}-failure "
                       f"reconstruct, {passes} passes in {el:.1f}s, C oracle (64-bit SWAR "
                       f"restatement of isa-l pq_gen_base + nibble-table gf_vect_mul), "
                       f"-O3 -mavx2, {threads} pthreads"}
@@ -98,9 +134,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
-    ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--strip-kib", type=int, default=64)
+    ap.add_argument("--config", default="raid6_8p2_64k", choices=sorted(CONFIGS))
+    ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (override)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -122,7 +157,9 @@ def main() -> None:
     ec.lib()
     ec.set_variant(args.variant)
 
-    k, m, S, B = args.k, 2, args.strip_kib * 1024, args.stripes
+    cfg = CONFIGS[args.config]
+    k, m, S = cfg["k"], cfg["m"], cfg["strip_kib"] * 1024
+    B = args.stripes or cfg["stripes"]
     n = k + m
     # Stripe-major layout in HBM: stripe s = [D0 .. D{k-1} P Q], strips contiguous.
     buf = torch.empty(B * n * S, dtype=torch.uint8, device=dev)
@@ -133,7 +170,9 @@ def main() -> None:
     base = buf.data_ptr()
     table = (base + torch.arange(B * n, dtype=torch.int64, device=dev) * S).contiguous()
     lo, hi = shard_range(B * world, rank, world)  # this rank's global stripe indices
-    fail = torch.from_numpy(failure_pairs(B, k, 0x1234 ^ lo).reshape(-1)).to(dev)
+    fgen = failure_pairs if cfg["failures"] == "dual" else failure_single
+    fail_np = fgen(B, k, 0x1234 ^ lo)
+    fail = torch.from_numpy(fail_np.reshape(-1)).to(dev)
     batch = ec.make_batch(k, m, S, B, table)
 
     stream = torch.cuda.current_stream(dev)
@@ -173,24 +212,41 @@ def main() -> None:
     if not args.no_verify:
         # erase the two failed data strips of every stripe, reconstruct, compare
         good = view[:, :k].clone()
-        f2 = fail.view(B, 2).long()
         si = torch.arange(B, device=dev)
-        view[si, f2[:, 0]] = 0
-        view[si, f2[:, 1]] = 0
+        for slot in range(2):
+            idx = np.nonzero(fail_np[:, slot] != 0xFF)[0]
+            if len(idx):
+                ii = torch.from_numpy(idx).to(dev)
+                view[si[ii], torch.from_numpy(fail_np[idx, slot].astype(np.int64)).to(dev)] = 0
         ec.reconstruct(batch, fail, sh)
         torch.cuda.synchronize(dev)
         verified = bool(torch.equal(view[:, :k], good))
         del good
 
     value = units / elapsed / GIB
-    workload = f"raid6_{k}p{m}_{S // 1024}k"
-    enc_bytes = float(n * S * B)          # algorithmic: k reads + 2 writes per stripe
-    rec_bytes = float(n * S * B)          # k-2 data + P + Q reads, 2 writes per stripe
+    workload = args.config
+    enc_bytes = float(n * S * B)  # algorithmic: k data read + m parity written per stripe
+    rec_bytes = float(reconstruct_bytes_per_stripe(k, m, S, cfg["failures"]) * B)
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_pmc_traffic(workload)
+    rec_gbs = rec_bytes / (rec_ms * 1e-3) / 1e9
+    pmc, pmc_src = load_pmc(workload)
+
+    def roof(kind, gbs, nbytes):
+        name = (f"k_encode<K={k},M={m}> (draid_ec_encode)" if kind == "encode" else
+                f"k_reconstruct<K={k},M={m}> (draid_ec_reconstruct, {cfg['failures']} failure)")
+        return {"bound": "hbm", "kernel": name, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                "traffic": (pmc or {}).get(f"{kind}_hbm_bytes_per_launch"),
+                "traffic_source": pmc_src, "algorithmic_bytes_per_launch": nbytes}
+
+    roofs = {"encode": roof("encode", enc_gbs, enc_bytes),
+             "reconstruct": roof("reconstruct", rec_gbs, rec_bytes)}
+    dominant = "reconstruct" if rec_ms >= enc_ms else "encode"
+    metric = ("GiB/s device-resident RAID6 8+2 encode+reconstruct, 64KiB strips, 1/2/4/8 GPU"
+              if workload == "raid6_8p2_64k" else f"GiB/s device-resident {cfg['label']}")
 
     out = {
-        "metric": "GiB/s device-resident RAID6 8+2 encode+reconstruct, 64KiB strips, 1/2/4/8 GPU",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -203,9 +259,9 @@ def main() -> None:
         "dtype": "u8",
         "data": "synthetic (uniform random bytes, torch Generator seed 0x1234+rank)",
         "config": {
-            "workload": f"RAID6 {k}+{m} P+Q encode + dual-data-failure reconstruct, "
-                        f"{S // 1024} KiB strips, {B} stripes per GPU (configs[2])",
-            "k": k, "m": m, "strip_bytes": S, "stripes_per_gpu": B,
+            "workload": f"{cfg['label']}, {B} stripes per GPU",
+            "name": workload, "k": k, "m": m, "strip_bytes": S, "stripes_per_gpu": B,
+            "failures": cfg["failures"],
             "layout": "stripe-major contiguous, device pointer table",
             "parallelism": f"stripe-sharded x{world}, no collectives",
         },
@@ -215,19 +271,10 @@ def main() -> None:
             "encode_user_gib_s": round(k * S * B / (enc_ms * 1e-3) / GIB, 1),
             "reconstruct_user_gib_s": round(k * S * B / (rec_ms * 1e-3) / GIB, 1),
             "encode_hbm_gb_s": round(enc_gbs, 1),
-            "reconstruct_hbm_gb_s": round(rec_bytes / (rec_ms * 1e-3) / 1e9, 1),
+            "reconstruct_hbm_gb_s": round(rec_gbs, 1),
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": f"k_encode<K={k},M=2> (draid_ec_encode)",
-            "achieved": round(enc_gbs, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "algorithmic_bytes_per_launch": enc_bytes,
-        },
+        "roofline": roofs[dominant],
+        "roofline_other": roofs["encode" if dominant == "reconstruct" else "reconstruct"],
         "verified_roundtrip": verified,
     }
     if rank == 0:
@@ -236,7 +283,8 @@ def main() -> None:
                 threads = min(16, len(os.sched_getaffinity(0)))
             except AttributeError:
                 threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(k, m, S, args.cpu_seconds, threads)
+            out["cpu_baseline"] = cpu_baseline(k, m, S, cfg["failures"], args.cpu_seconds,
+                                               threads)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

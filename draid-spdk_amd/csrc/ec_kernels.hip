@@ -345,10 +345,12 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
     using MW = Mem<W>;
     const uint8_t* pP = pp.get(s, k);
     const uint8_t* pQ = (M == 2) ? pp.get(s, k + 1) : pP;
-    // A strip that is lost (or not needed) is loaded from `sub` instead -- an
-    // address this lane loads anyway, so the duplicate is a cache hit -- and
-    // masked to zero.  That keeps every load unconditional and batched.
-    const uint8_t* sub = pl.lostP ? pQ : pP;
+    // Lost (or unneeded) strips are skipped with wave-uniform branches: their
+    // pointers stay scalar, no load depends on another, and every surviving
+    // load of the lane is in flight before the first XOR.  (Re-pointing a lost
+    // strip at an address already loaded lets the compiler forward that value,
+    // which makes every later load wait for it.)
+    const bool useP = !pl.lostP;
     const bool useQ = pl.needq && !pl.lostQ;
     W ps[U], qs[U], pv[U], qv[U];
     bool ok[U];
@@ -357,19 +359,21 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
         ok[u] = !BOUNDED || i0 + u * stride < n;
         ps[u] = W(0);
         qs[u] = W(0);
-        pv[u] = ok[u] ? MW::template ld<(POL & 1) != 0>(pl.lostP ? sub : pP, i0 + u * stride) : W(0);
-        qv[u] = ok[u] ? MW::template ld<(POL & 1) != 0>(useQ ? pQ : sub, i0 + u * stride) : W(0);
+        pv[u] = (useP && ok[u]) ? MW::template ld<(POL & 1) != 0>(pP, i0 + u * stride) : W(0);
+        qv[u] = (useQ && ok[u]) ? MW::template ld<(POL & 1) != 0>(pQ, i0 + u * stride) : W(0);
     }
     for_sources_desc<KT>(k, [&](int j) {
-        const bool dead = (j == pl.x) || (j == pl.y);
-        const uint8_t* src = dead ? sub : pp.get(s, j);
-        const uint32_t keep = dead ? 0u : 0xffffffffu;
+        const bool live = (j != pl.x) && (j != pl.y);
+        W d[U];
+        const uint8_t* src = pp.get(s, j);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            d[u] = (live && ok[u]) ? MW::template ld<(POL & 1) != 0>(src, i0 + u * stride) : W(0);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const W d = (ok[u] ? MW::template ld<(POL & 1) != 0>(src, i0 + u * stride) : W(0)) & keep;
-            ps[u] ^= d;
+            ps[u] ^= d[u];
             if constexpr (M == 2)
-                qs[u] = gf_mul2(qs[u]) ^ d;
+                qs[u] = gf_mul2(qs[u]) ^ d[u];
         }
     });
     constants(pl);
@@ -431,10 +435,17 @@ __device__ __forceinline__ void reconstruct_item(const Ptrs& pp, uint32_t s, uin
     auto none = [](RecPlan&) {};
     if (stripe_aligned<KT, M>(pp, s, k)) {
         const uint32_t i0 = c * EPB + threadIdx.x;
-        if ((c + 1) * EPB <= nvec)
+        if ((c + 1) * EPB <= nvec) {
             recover_elems<KT, M, U, POL, false, u32x4>(pp, s, k, pl, i0, NTHR, nvec, constants);
-        else
-            recover_elems<KT, M, U, POL, true, u32x4>(pp, s, k, pl, i0, NTHR, nvec, constants);
+        } else {
+            // Partial last chunk (rare): one vector at a time keeps this path's
+            // registers below the main path's, so it does not cap occupancy.
+            constants(pl);
+#pragma unroll 1
+            for (int u = 0; u < U; ++u)
+                recover_elems<KT, M, 1, POL, true, u32x4>(pp, s, k, pl, i0 + u * NTHR, NTHR, nvec,
+                                                          none);
+        }
         const uint32_t tail = len & 15u;
         if (tail && c == cps - 1 && threadIdx.x < tail)
             recover_elems<0, M, 1, 0, true, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
@@ -459,6 +470,21 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
     const uint32_t total = cps * nstripes;
     if constexpr (C::MAP == 2)
         stage_gf_tables<C::NTHR>(lds);  // once per persistent workgroup
+    // The table word this lane stages is loaded FIRST: vmcnt retires in issue
+    // order, so the LDS write below then waits only for it, not for the strip
+    // loads issued after it -- staging and barrier overlap the strip loads.
+    constexpr int kTabWords = (512 + 256) / 4;
+    constexpr int kPerLane = (kTabWords + C::NTHR - 1) / C::NTHR;
+    uint32_t tab_word[kPerLane];
+#pragma unroll
+    for (int w = 0; w < kPerLane; ++w) {
+        const int t = threadIdx.x + w * C::NTHR;
+        tab_word[w] = 0;
+        if constexpr (C::MAP != 2 && C::PLAN == 0) {
+            if (t < kTabWords)
+                tab_word[w] = reinterpret_cast<const uint32_t*>(&c_gf)[t];
+        }
+    }
     for (uint32_t b = blockIdx.x; b < total; b += (C::MAP == 2 ? gridDim.x : total)) {
         uint32_t s, c;
         item_coords<C>(b, cps, nstripes, s, c);
@@ -470,7 +496,14 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
         RecPlan pl = decode_failures<M>(k, f0, f1);
         if (pl.skip)
             continue;  // uniform across the workgroup
-        if constexpr (C::PLAN == 1) {
+        if constexpr (C::PLAN == 2) {
+            // DIAGNOSTIC ONLY (tools/sweep.py): constants left zero, no LDS, no
+            // barrier -- wrong results, measures what the plan step costs.
+            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
+                p.t1 = make_nib_table(0);
+                p.t2 = make_nib_table(0);
+            });
+        } else if constexpr (C::PLAN == 1) {
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
                 plan_constants(p, c_gf.exp, c_gf.log);
             });
@@ -481,7 +514,13 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
         } else {
             // Stage the tables while this lane's strip loads are in flight.
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-                stage_gf_tables<C::NTHR>(lds);
+#pragma unroll
+                for (int w = 0; w < kPerLane; ++w) {
+                    const int t = threadIdx.x + w * C::NTHR;
+                    if (t < kTabWords)
+                        lds.w[t] = tab_word[w];
+                }
+                __syncthreads();
                 plan_constants(p, l_exp, l_log);
             });
         }
@@ -560,13 +599,14 @@ __global__ __launch_bounds__(kThreads) void k_gf_vect_mul(const uint8_t* src, ui
 
 // ------------------------------------------------------------ launchers
 
-// Vectors per lane per strip (measured with tools/sweep.py at 8+2 x 64 KiB):
-// encode is fastest at U=1 (6.43 TB/s vs 6.20 at U=2); reconstruct at U=2
-// (6.14 vs 5.81 TB/s), where a workgroup also stages the GF tables and derives
-// its constants, so more bytes per workgroup amortise that.  Fewer sources keep
-// more vectors so a lane still issues >= 8 loads.
-constexpr int enc_unroll(int k) { return k <= 4 ? 2 : 1; }
-constexpr int rec_unroll(int k) { return k <= 8 ? 2 : 1; }
+// Vectors per lane per strip, measured with tools/sweep.py: U=1 is fastest for
+// both kernels at every BASELINE shape (8+2 x 64 KiB encode 6.44 TB/s vs 6.24 at
+// U=2; reconstruct 6.30 vs 5.86; 4+1 encode 6.22 vs 5.89).  Small workgroups
+// turn over quickly, and with the GF-table staging issued ahead of the strip
+// loads the reconstruct plan step costs nothing measurable at U=1 (6.296 vs a
+// no-plan diagnostic build's 6.297 TB/s).
+constexpr int enc_unroll(int) { return 1; }
+constexpr int rec_unroll(int) { return 1; }
 
 static inline uint32_t chunks_per_stripe(uint64_t len, int nthr, int U)
 {
@@ -686,35 +726,45 @@ using V9 = Cfg<64, 1, 3, 0, 0>;    // one wave
 using V10 = Cfg<256, 1, 3, 0, 0>;  // U=1
 using V11 = Cfg<512, 2, 3, 0, 0>;  // 512 lanes, U=2
 using V12 = Cfg<256, 4, 3, 0, 0>;  // U=4
+using V13 = Cfg<256, 2, 3, 0, 2>;  // DIAGNOSTIC: reconstruct without the plan step, U=2
+using V14 = Cfg<256, 1, 3, 0, 2>;  // DIAGNOSTIC: reconstruct without the plan step, U=1
 #define DRAID_VARIANTS(X) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5) X(6, V6) X(7, V7) X(8, V8) \
-    X(9, V9) X(10, V10) X(11, V11) X(12, V12)
+    X(9, V9) X(10, V10) X(11, V11) X(12, V12) X(13, V13) X(14, V14)
 
-static hipError_t variant_encode_8p2(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
-                                     hipStream_t st)
+template <int K, int M>
+static hipError_t variant_encode(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
+                                 hipStream_t st)
 {
     switch (v) {
 #define DRAID_V(N, C) \
     case N:           \
-        return go_encode<8, 2, false, C>(pp, 8, len, ns, nullptr, st);
+        return go_encode<K, M, false, C>(pp, K, len, ns, nullptr, st);
         DRAID_VARIANTS(DRAID_V)
 #undef DRAID_V
     default:
-        return go_encode<8, 2, false, CfgDefault<enc_unroll(8)>>(pp, 8, len, ns, nullptr, st);
+        return go_encode<K, M, false, CfgDefault<enc_unroll(K)>>(pp, K, len, ns, nullptr, st);
     }
 }
 
-static hipError_t variant_reconstruct_8p2(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
-                                          const uint8_t* fail, hipStream_t st)
+template <int K, int M>
+static hipError_t variant_reconstruct(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
+                                      const uint8_t* fail, hipStream_t st)
 {
     switch (v) {
 #define DRAID_V(N, C) \
     case N:           \
-        return go_reconstruct<8, 2, C>(pp, 8, len, ns, fail, 0xffffu, st);
+        return go_reconstruct<K, M, C>(pp, K, len, ns, fail, 0xffffu, st);
         DRAID_VARIANTS(DRAID_V)
 #undef DRAID_V
     default:
-        return go_reconstruct<8, 2, CfgDefault<rec_unroll(8)>>(pp, 8, len, ns, fail, 0xffffu, st);
+        return go_reconstruct<K, M, CfgDefault<rec_unroll(K)>>(pp, K, len, ns, fail, 0xffffu, st);
     }
+}
+
+// Sweep hook: variants exist for the BASELINE shapes 4+1, 8+2 and 16+2.
+static bool has_variants(uint32_t k, uint32_t m)
+{
+    return (k == 4 && m == 1) || (k == 8 && m == 2) || (k == 16 && m == 2);
 }
 
 hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
@@ -722,8 +772,10 @@ hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes
 {
     if (table) {
         const TablePtrs pp{table, k + m};
-        if (g_variant != 0 && k == 8 && m == 2)
-            return variant_encode_8p2(g_variant, pp, len, nstripes, st);
+        if (g_variant != 0 && has_variants(k, m))
+            return k == 4 ? variant_encode<4, 1>(g_variant, pp, len, nstripes, st)
+                 : k == 8 ? variant_encode<8, 2>(g_variant, pp, len, nstripes, st)
+                          : variant_encode<16, 2>(g_variant, pp, len, nstripes, st);
         if (m == 1)
             return dispatch_encode<1>(pp, k, len, nstripes, st);
         return dispatch_encode<2>(pp, k, len, nstripes, st);
@@ -741,8 +793,10 @@ hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nst
     const uint32_t f01 = static_cast<uint32_t>(f0) | (static_cast<uint32_t>(f1) << 8);
     if (table) {
         const TablePtrs pp{table, k + m};
-        if (g_variant != 0 && k == 8 && m == 2 && fail_dev)
-            return variant_reconstruct_8p2(g_variant, pp, len, nstripes, fail_dev, st);
+        if (g_variant != 0 && has_variants(k, m) && fail_dev)
+            return k == 4 ? variant_reconstruct<4, 1>(g_variant, pp, len, nstripes, fail_dev, st)
+                 : k == 8 ? variant_reconstruct<8, 2>(g_variant, pp, len, nstripes, fail_dev, st)
+                          : variant_reconstruct<16, 2>(g_variant, pp, len, nstripes, fail_dev, st);
         if (m == 1)
             return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, f01, st);
         return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, f01, st);

@@ -22,7 +22,8 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = {0: "default (enc U1, rec U2)", 1: "U2", 2: "512 lanes U1", 3: "128 lanes",
             4: "chunk-major map", 5: "persistent", 6: "scalar plan", 7: "persist 512 scalar",
-            8: "1024 lanes", 9: "64 lanes", 10: "U1", 11: "512 lanes U2", 12: "U4"}
+            8: "1024 lanes", 9: "64 lanes", 10: "U1", 11: "512 lanes U2", 12: "U4",
+            13: "DIAG no-plan U2", 14: "DIAG no-plan U1"}
 
 
 def probe(torch, dev, nbytes, rounds, iters):
@@ -87,6 +88,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--strip-kib", type=int, default=64)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--failures", default="dual", choices=["dual", "single"])
     ap.add_argument("--layouts", default="stripe_major,stripe_major_gap256,stripe_major_gap4096,strip_major")
     ap.add_argument("--variants", default="0,1,2,8,10,11,12")
     ap.add_argument("--probe", action="store_true")
@@ -98,9 +101,11 @@ def main():
     import bench
 
     dev = torch.device("cuda", 0)
-    k, m, S, B = 8, 2, args.strip_kib * 1024, args.stripes
+    k, S, B = args.k, args.strip_kib * 1024, args.stripes
+    m = 1 if k == 4 else 2
     probes = probe(torch, dev, (k + m) * S * B, args.rounds, args.iters) if args.probe else []
-    fail = torch.from_numpy(bench.failure_pairs(B, k, 0x1234).reshape(-1)).to(dev)
+    fgen = bench.failure_pairs if args.failures == "dual" else bench.failure_single
+    fail = torch.from_numpy(fgen(B, k, 0x1234).reshape(-1)).to(dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     layouts = {}
@@ -110,6 +115,7 @@ def main():
     variants = [int(v) for v in args.variants.split(",")]
     res = {f"{l}|{v}|{op}": [] for l in layouts for v in variants for op in ("enc", "rec")}
     nbytes = (k + m) * S * B
+    rec_nbytes = bench.reconstruct_bytes_per_stripe(k, m, S, args.failures) * B
     for r in range(args.rounds):
         for lname, (_, _, batch) in layouts.items():
             for v in variants:
@@ -134,7 +140,8 @@ def main():
         med = float(np.median(vals))
         summary.append({"layout": lname, "variant": int(v), "desc": VARIANTS[int(v)], "op": op,
                         "median_us": round(med, 2), "min_us": round(min(vals), 2),
-                        "hbm_gb_s": round(nbytes / (med * 1e-6) / 1e9, 1)})
+                        "hbm_gb_s": round((nbytes if op == "enc" else rec_nbytes) / (med * 1e-6)
+                                          / 1e9, 1)})
     summary.sort(key=lambda d: (d["op"], d["median_us"]))
     for d in summary:
         print(f'{d["op"]} {d["layout"]:24s} v{d["variant"]} {d["desc"]:22s} '
