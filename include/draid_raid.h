@@ -1,0 +1,116 @@
+/*
+ * draid_raid.h -- host-side RAID5/RAID6 stripe layer over the draid_ec C ABI.
+ *
+ * The SPDK-independent part of a raid level module (module/bdev/raid/raid5.c,
+ * raid5_simple.c): array geometry, parity placement, mapping a stripe request
+ * onto chunks, slicing the parent I/O's iovecs per chunk, and the full-stripe
+ * write / degraded read drivers that hand the parity arithmetic to the GPU
+ * through a draid_ec_ctx.  A real SPDK module wraps these
+ * calls with spdk_bdev_io / io_channel / poller glue; everything here is plain C
+ * on host memory that the GPU can reach (registered or device memory).
+ */
+#ifndef DRAID_RAID_H
+#define DRAID_RAID_H
+
+#include <stdbool.h>
+#include <stdint.h>
+#include <sys/uio.h>
+
+#include "draid_ec.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRAID_RAID_MAX_BASE 32
+#define DRAID_RAID_MAX_IOV 64
+
+/* struct raid_bdev / raid5_info fields the data path needs (bdev_raid.h:96-160,
+ * raid5.c:113-135). */
+struct draid_raid {
+    uint8_t level;            /* 5 or 6 */
+    uint8_t num_base_bdevs;   /* n */
+    uint8_t max_degraded;     /* parity strips per stripe: 1 (RAID5), 2 (RAID6) */
+    uint32_t blocklen;        /* bytes per block */
+    uint32_t strip_size;      /* blocks per strip (power of two) */
+    uint32_t strip_size_shift;
+    uint64_t stripe_blocks;   /* data blocks per stripe */
+    uint64_t total_stripes;
+    uint64_t blockcnt;        /* exported capacity in blocks */
+    uint64_t optimal_io_boundary;
+    uint32_t degraded_mask;   /* bit d set: base bdev d is degraded (bdev_raid.h:91-92) */
+};
+
+/* raid5_start geometry (raid5.c:1399-1426), generalised to m parity strips.
+ * Returns 0 or -EINVAL (n too small for the level, strip not a power of two). */
+int draid_raid_start(struct draid_raid *r, int level, int num_base_bdevs, uint32_t blocklen,
+                     uint32_t strip_size_blocks, uint64_t min_base_blockcnt);
+
+/* Parity placement.  RAID5: p = (n-1) - s mod n (raid5.c:1006-1007).  RAID6
+ * (undefined by the reference): p as RAID5, q = (p+1) mod n.
+ * Data indices fill the remaining disks in ascending order. */
+void draid_raid_parity_chunks(const struct draid_raid *r, uint64_t stripe, int *p, int *q);
+int draid_raid_data_disk(const struct draid_raid *r, uint64_t stripe, int data_idx);
+int draid_raid_disk_data_index(const struct draid_raid *r, uint64_t stripe, int disk); /* -1 for P/Q */
+
+/* Per-chunk request of a stripe request (struct chunk, raid5.c:52-88). */
+struct draid_chunk_req {
+    uint64_t req_offset;      /* blocks from the chunk start */
+    uint64_t req_blocks;
+};
+
+/* raid5_handle_stripe (raid5.c:962-1055): maps [stripe_offset, +blocks) of one
+ * stripe onto its chunks.  chunk[] is indexed by base bdev. */
+struct draid_stripe_req {
+    uint64_t stripe_index;
+    int p_disk, q_disk;       /* q_disk = -1 for RAID5 */
+    int first_data, last_data;/* data indices touched */
+    bool full_stripe;
+    struct draid_chunk_req chunk[DRAID_RAID_MAX_BASE];
+};
+
+int draid_raid_map_request(const struct draid_raid *r, uint64_t offset_blocks,
+                           uint64_t num_blocks, struct draid_stripe_req *out);
+
+/* raid5_chunk_map_iov (raid5.c:358-426): the iovecs covering [offset, offset+len)
+ * of a parent iovec list.  Returns the iovec count, or -EINVAL / -ENOSPC. */
+int draid_raid_map_iov(struct iovec *out, int out_max, const struct iovec *iov, int iovcnt,
+                       uint64_t offset, uint64_t len);
+
+/* One base-bdev I/O the module must issue (spdk_bdev_{read,write}v_blocks,
+ * raid5.c:617-662): base LBA = stripe * strip_size + offset (raid5.c:648). */
+struct draid_base_io {
+    int disk;
+    uint64_t offset_blocks;
+    uint64_t num_blocks;
+    int iovcnt;
+    struct iovec iov[DRAID_RAID_MAX_IOV];
+};
+
+/* Full-stripe write (raid5_stripe_write_preread_complete / raid5_xor_stripe):
+ * slices the parent iovecs into the k data chunks, queues the parity encode into
+ * parity_buf[0] (P) and parity_buf[1] (Q, RAID6) on ctx, and fills writes[0..n)
+ * with every base write to issue once the ctx has completed (after
+ * draid_ec_ctx_flush + query/synchronize).  Non-full-stripe requests are
+ * rejected with -EINVAL, as raid5_simple does (raid5_simple.c:381-395). */
+int draid_raid_stripe_write(const struct draid_raid *r, draid_ec_ctx *ctx,
+                            const struct draid_stripe_req *req, const struct iovec *iov,
+                            int iovcnt, void *const parity_buf[2],
+                            struct draid_base_io *writes, int *nwrites);
+
+/* Degraded read of a whole stripe (raid5_stripe_read + the reconstruct of
+ * raid5_complete_reconstructed_stripe_request, raid5.c:544-594,869-946,
+ * generalised to two failures): `chunk_buf[disk]` are the stripe's per-disk
+ * buffers (strip bytes each) that the caller fills with the surviving base
+ * reads listed in reads[]; the reconstruct of the degraded chunks into
+ * chunk_buf is queued on ctx; afterwards the caller copies data chunks out (or
+ * passes chunk_buf of data disks = the user's buffers).  -EIO if more disks are
+ * degraded than the level tolerates. */
+int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                    uint64_t stripe, void *const *chunk_buf,
+                                    struct draid_base_io *reads, int *nreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRAID_RAID_H */

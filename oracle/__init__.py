@@ -19,8 +19,9 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "isal_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("isal_oracle.c", "bdevperf_raid5.c", "isal_oracle.h")]
+    if force or not os.path.exists(LIB_PATH) or \
+            os.path.getmtime(LIB_PATH) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
     return LIB_PATH
 
@@ -62,6 +63,9 @@ def lib() -> C.CDLL:
         L.orc_glibc_rand_buffer.argtypes = [vp, C.c_long]
         L.orc_fill_splitmix.argtypes = [vp, sz, C.c_uint64]
         L.orc_fill_ut_ref_pattern.argtypes = [vp, C.c_uint64, u32]
+        L.orc_bdevperf_raid5_fsw.restype = C.c_double
+        L.orc_bdevperf_raid5_fsw.argtypes = [i32, sz, sz, C.c_double, C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_ubyte)]
         _lib = L
     return _lib
 
@@ -191,3 +195,12 @@ def bench_encode_reconstruct(buf: np.ndarray, k: int, m: int, length: int, nstri
                                             int(with_reconstruct), nthreads, min_seconds,
                                             C.byref(passes))
     return el, passes.value
+
+
+def bdevperf_raid5_fsw(n: int = 5, strip: int = 65536, disk_bytes: int = 256 << 20,
+                       seconds: float = 10.0):
+    """BASELINE config 1 CPU harness: (MiB/s, ios, verified)."""
+    ios = C.c_uint64()
+    ok = C.c_ubyte()
+    mibs = lib().orc_bdevperf_raid5_fsw(n, strip, disk_bytes, seconds, C.byref(ios), C.byref(ok))
+    return mibs, ios.value, bool(ok.value)

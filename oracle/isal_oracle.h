@@ -67,6 +67,10 @@ double orc_bench_encode_reconstruct(int k, int m, size_t len, uint32_t nstripes,
                                     int with_reconstruct, int nthreads,
                                     double min_seconds, uint64_t *passes);
 
+/* ---- BASELINE config 1 CPU harness (bdevperf_raid5.c) ---- */
+double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, double seconds,
+                              uint64_t *ios_out, uint8_t *verify_ok);
+
 /* ---- reference RAID5 geometry (module/bdev/raid/raid5.c) ---- */
 int  orc_raid5_parity_chunk(int num_base_bdevs, int max_degraded, uint64_t stripe_index);
 int  orc_raid5_data_chunk_to_disk(int parity_chunk, int data_idx);

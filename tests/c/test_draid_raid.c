@@ -1,0 +1,310 @@
+/*
+ * test_draid_raid.c -- C tests of the host RAID layer over libdraid_ec.so,
+ * modelled on the reference's unit tests:
+ *   - raid5_ut.c:61-105,176-195: geometry over n x blockcnt x blocklen x strip grid
+ *   - raid5_ut_ref.c:284-397,489-512: full-stripe writes of the 0xFF + block-index
+ *     pattern through fake base bdevs that memcpy each base write into a buffer,
+ *     parity checked against the oracle; non-full-stripe writes must fail.
+ *   - degraded reads with every single (RAID5/6) and double (RAID6) failure.
+ * `--cpu-only` runs only the host logic (geometry, request and iovec mapping).
+ */
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "draid_ec.h"
+#include "draid_raid.h"
+#include "isal_oracle.h"
+
+static int g_fail;
+#define CHECK(c)                                                                   \
+    do {                                                                           \
+        if (!(c)) {                                                                \
+            fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+            g_fail++;                                                              \
+        }                                                                          \
+    } while (0)
+#define HIPOK(x)                                                                         \
+    do {                                                                                 \
+        int _rc = (x);                                                                   \
+        if (_rc) {                                                                       \
+            fprintf(stderr, "%s:%d: %s -> %d (%s)\n", __FILE__, __LINE__, #x, _rc,       \
+                    draid_ec_last_error());                                              \
+            exit(2);                                                                     \
+        }                                                                                \
+    } while (0)
+
+/* raid5_ut.c:176-195, generalised to RAID6 */
+static void test_geometry(void)
+{
+    const int levels[] = {5, 6};
+    const int ns[] = {3, 4, 5, 6, 10};
+    const uint64_t blockcnts[] = {1, 1024, 1024 * 1024};
+    const uint32_t bls[] = {512, 4096};
+    const uint32_t skbs[] = {1, 4, 128};
+    for (unsigned a = 0; a < 2; a++)
+        for (unsigned b = 0; b < 5; b++)
+            for (unsigned c = 0; c < 3; c++)
+                for (unsigned d = 0; d < 2; d++)
+                    for (unsigned e = 0; e < 3; e++) {
+                        const int lvl = levels[a], n = ns[b], m = lvl == 6 ? 2 : 1;
+                        const uint32_t strip = skbs[e] * 1024 / bls[d];
+                        if (strip == 0 || strip > blockcnts[c])
+                            continue;
+                        struct draid_raid r;
+                        int rc = draid_raid_start(&r, lvl, n, bls[d], strip, blockcnts[c]);
+                        if (n < m + 2) {
+                            CHECK(rc == -EINVAL);
+                            continue;
+                        }
+                        CHECK(rc == 0);
+                        CHECK(r.stripe_blocks == (uint64_t)strip * (n - m));
+                        CHECK(r.total_stripes == blockcnts[c] / strip);
+                        CHECK(r.blockcnt == (blockcnts[c] - blockcnts[c] % strip) * (n - m));
+                        CHECK(r.optimal_io_boundary == r.stripe_blocks);
+                        if (lvl == 5) { /* agrees with the oracle's restatement of raid5.c */
+                            uint64_t sb, ts, bc, oib;
+                            orc_raid5_start_geometry(n, 1, blockcnts[c], strip, &sb, &ts, &bc,
+                                                     &oib);
+                            CHECK(sb == r.stripe_blocks && ts == r.total_stripes &&
+                                  bc == r.blockcnt && oib == r.optimal_io_boundary);
+                        }
+                    }
+    struct draid_raid r;
+    CHECK(draid_raid_start(&r, 5, 4, 512, 3, 1024) == -EINVAL); /* strip not a power of 2 */
+    CHECK(draid_raid_start(&r, 0, 4, 512, 8, 1024) == -EINVAL);
+}
+
+/* Parity placement and the ut_ref request list (raid5_ut_ref.c:436-452). */
+static void test_mapping(void)
+{
+    for (int lvl = 5; lvl <= 6; lvl++)
+        for (int n = lvl == 5 ? 3 : 4; n <= 10; n++) {
+            struct draid_raid r;
+            const uint32_t strip = 8;
+            CHECK(draid_raid_start(&r, lvl, n, 512, strip, 64 * strip) == 0);
+            const int m = r.max_degraded, k = n - m;
+            for (uint64_t s = 0; s < (uint64_t)2 * n; s++) {
+                int p, q;
+                draid_raid_parity_chunks(&r, s, &p, &q);
+                if (lvl == 5) {
+                    CHECK(p == orc_raid5_parity_chunk(n, 1, s));
+                    for (int d = 0; d < k; d++)
+                        CHECK(draid_raid_data_disk(&r, s, d) == orc_raid5_data_chunk_to_disk(p, d));
+                } else {
+                    CHECK(q == (p + 1) % n);
+                }
+                int seen[DRAID_RAID_MAX_BASE] = {0};
+                for (int d = 0; d < k; d++) {
+                    const int disk = draid_raid_data_disk(&r, s, d);
+                    CHECK(disk >= 0 && disk != p && disk != q && !seen[disk]);
+                    seen[disk] = 1;
+                    CHECK(draid_raid_disk_data_index(&r, s, disk) == d);
+                }
+                CHECK(draid_raid_disk_data_index(&r, s, p) == -1);
+            }
+            const uint64_t sb = r.stripe_blocks;
+            const uint64_t reqs[][2] = {{0, 1}, {0, strip}, {0, strip + 1}, {0, sb},
+                                        {1, 1}, {1, strip}, {1, strip + 1}, {strip, 1},
+                                        {strip, strip}, {strip - 1, 1}, {strip - 1, strip},
+                                        {strip - 1, 2}};
+            for (unsigned i = 0; i < sizeof(reqs) / sizeof(reqs[0]); i++) {
+                for (uint64_t s = 0; s < (uint64_t)n; s++) {
+                    struct draid_stripe_req q;
+                    const uint64_t off = s * sb + reqs[i][0], len = reqs[i][1];
+                    if (reqs[i][0] + len > sb) {
+                        CHECK(draid_raid_map_request(&r, off, len, &q) == -EINVAL);
+                        continue;
+                    }
+                    CHECK(draid_raid_map_request(&r, off, len, &q) == 0);
+                    uint64_t total = 0;
+                    for (int disk = 0; disk < n; disk++) {
+                        total += q.chunk[disk].req_blocks;
+                        CHECK(q.chunk[disk].req_offset + q.chunk[disk].req_blocks <= strip);
+                    }
+                    CHECK(total == len);
+                    CHECK(q.chunk[q.p_disk].req_blocks == 0);
+                    CHECK(q.full_stripe == (reqs[i][0] == 0 && len == sb));
+                    /* the first touched chunk starts at the request offset */
+                    const int fd = draid_raid_data_disk(&r, s, q.first_data);
+                    CHECK(q.chunk[fd].req_offset == reqs[i][0] % strip);
+                }
+            }
+        }
+    /* raid5_chunk_map_iov over an uneven parent list */
+    uint8_t buf[100];
+    struct iovec par[3] = {{buf, 10}, {buf + 10, 0}, {buf + 10, 90}}, out[4];
+    /* a zero-length iovec inside the range is kept, as raid5.c:384-391 counts it */
+    CHECK(draid_raid_map_iov(out, 4, par, 3, 5, 20) == 3);
+    CHECK(out[0].iov_base == buf + 5 && out[0].iov_len == 5);
+    CHECK(out[1].iov_len == 0);
+    CHECK(out[2].iov_base == buf + 10 && out[2].iov_len == 15);
+    CHECK(draid_raid_map_iov(out, 4, par, 3, 10, 90) == 1);
+    CHECK(draid_raid_map_iov(out, 4, par, 3, 95, 10) == -EINVAL);
+    CHECK(draid_raid_map_iov(out, 1, par, 3, 0, 20) == -ENOSPC);
+    CHECK(draid_raid_map_iov(out, 4, par, 3, 0, 10) == 1);
+}
+
+/* ---------------------------------------------------------------- GPU tests */
+
+static void d2d(void *dst, const void *src, size_t n, void *st)
+{
+    HIPOK(draid_ec_memcpy_async(dst, src, n, 2, st));
+}
+
+static int cmp_host(const uint8_t *a, const uint8_t *b, size_t n) { return memcmp(a, b, n) == 0; }
+
+static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
+{
+    struct draid_raid r;
+    const uint32_t strip = strip_kb * 1024 / blocklen;
+    const uint64_t nstripes = (uint64_t)n + 1;
+    CHECK(draid_raid_start(&r, lvl, n, blocklen, strip, strip * nstripes) == 0);
+    const int m = r.max_degraded, k = n - m;
+    const size_t sb = (size_t)strip * blocklen, disk_bytes = sb * r.total_stripes;
+    const size_t ub = (size_t)r.stripe_blocks * blocklen;
+
+    draid_ec_ctx *ctx;
+    HIPOK(draid_ec_ctx_create(&ctx));
+    void *st = draid_ec_ctx_stream(ctx);
+    uint8_t *disk[DRAID_RAID_MAX_BASE], *user, *pbuf[2], *chunk[DRAID_RAID_MAX_BASE], *junk;
+    for (int d = 0; d < n; d++) {
+        HIPOK(draid_ec_device_alloc((void **)&disk[d], disk_bytes));
+        HIPOK(draid_ec_device_alloc((void **)&chunk[d], sb));
+    }
+    HIPOK(draid_ec_device_alloc((void **)&user, ub * r.total_stripes));
+    HIPOK(draid_ec_device_alloc((void **)&pbuf[0], sb));
+    HIPOK(draid_ec_device_alloc((void **)&pbuf[1], sb));
+    HIPOK(draid_ec_device_alloc((void **)&junk, sb));
+
+    /* user data: the raid5_ut_ref pattern, one new payload per stripe */
+    uint8_t *hu = malloc(ub * r.total_stripes), *hj = malloc(sb);
+    for (uint64_t s = 0; s < r.total_stripes; s++) {
+        orc_fill_ut_ref_pattern(hu + s * ub, r.stripe_blocks, blocklen);
+        hu[s * ub + 9] = (uint8_t)s;
+    }
+    memset(hj, 0xA5, sb);
+    HIPOK(draid_ec_memcpy_async(user, hu, ub * r.total_stripes, 0, st));
+    HIPOK(draid_ec_memcpy_async(junk, hj, sb, 0, st));
+
+    for (uint64_t s = 0; s < r.total_stripes; s++) {
+        struct draid_stripe_req q;
+        CHECK(draid_raid_map_request(&r, s * r.stripe_blocks, r.stripe_blocks, &q) == 0);
+        CHECK(q.full_stripe);
+        /* the parent I/O arrives as three uneven iovecs */
+        uint8_t *u = user + s * ub;
+        const size_t a = ub / 3 + 7, b = ub / 5 + 1;
+        struct iovec iov[3] = {{u, a}, {u + a, b}, {u + a + b, ub - a - b}};
+        struct draid_base_io w[DRAID_RAID_MAX_BASE];
+        int nw = 0;
+        void *pq[2] = {pbuf[0], pbuf[1]};
+        CHECK(draid_raid_stripe_write(&r, ctx, &q, iov, 3, pq, w, &nw) == 0);
+        CHECK(nw == n);
+        HIPOK(draid_ec_ctx_flush(ctx));
+        /* fake base bdevs: memcpy every base write (raid5_ut_ref.c:284-323) */
+        for (int i = 0; i < nw; i++) {
+            size_t off = (size_t)w[i].offset_blocks * blocklen;
+            for (int v = 0; v < w[i].iovcnt; v++) {
+                d2d(disk[w[i].disk] + off, w[i].iov[v].iov_base, w[i].iov[v].iov_len, st);
+                off += w[i].iov[v].iov_len;
+            }
+            CHECK(off == (size_t)(w[i].offset_blocks + w[i].num_blocks) * blocklen);
+        }
+        HIPOK(draid_ec_ctx_synchronize(ctx));
+        /* non-full-stripe writes are rejected (raid5_ut_ref.c:489-512) */
+        struct draid_stripe_req pr;
+        CHECK(draid_raid_map_request(&r, s * r.stripe_blocks + 1, strip, &pr) == 0);
+        CHECK(draid_raid_stripe_write(&r, ctx, &pr, iov, 3, pq, w, &nw) == -EINVAL);
+    }
+
+    /* every stripe on the fake disks: data in place, parity == oracle */
+    uint8_t *hd[DRAID_RAID_MAX_BASE];
+    for (int d = 0; d < n; d++) {
+        hd[d] = malloc(disk_bytes);
+        HIPOK(draid_ec_memcpy_async(hd[d], disk[d], disk_bytes, 1, st));
+    }
+    HIPOK(draid_ec_ctx_synchronize(ctx));
+    uint8_t *ref = malloc(sb * 2);
+    for (uint64_t s = 0; s < r.total_stripes; s++) {
+        int p, qd;
+        draid_raid_parity_chunks(&r, s, &p, &qd);
+        void *vec[DRAID_RAID_MAX_BASE + 2];
+        for (int d = 0; d < k; d++) {
+            const int disk_i = draid_raid_data_disk(&r, s, d);
+            CHECK(cmp_host(hd[disk_i] + s * sb, hu + s * ub + d * sb, sb));
+            vec[d] = hu + s * ub + d * sb;
+        }
+        vec[k] = ref;
+        vec[k + 1] = ref + sb;
+        CHECK((m == 1 ? orc_xor_gen(k + 1, (int)sb, vec) : orc_pq_gen(k + 2, (int)sb, vec)) == 0);
+        CHECK(cmp_host(hd[p] + s * sb, ref, sb));
+        if (m == 2)
+            CHECK(cmp_host(hd[qd] + s * sb, ref + sb, sb));
+    }
+
+    /* degraded reads: every single failure, and every double failure for RAID6 */
+    uint8_t *hc = malloc(sb);
+    for (int f0 = 0; f0 < n; f0++)
+        for (int f1 = (m == 2 ? f0 : n); f1 <= n; f1++) {
+            if (f1 == f0 && f1 != n)
+                continue;
+            r.degraded_mask = (1u << f0) | (f1 < n ? (1u << f1) : 0);
+            const uint64_t s = (uint64_t)(f0 + f1) % r.total_stripes;
+            struct draid_base_io rd[DRAID_RAID_MAX_BASE];
+            int nr = 0;
+            for (int d = 0; d < n; d++)
+                d2d(chunk[d], junk, sb, st); /* degraded chunks start as garbage */
+            CHECK(draid_raid_stripe_degraded_read(&r, ctx, s, (void *const *)chunk, rd, &nr) == 0);
+            CHECK(nr == n - (f1 < n ? 2 : 1));
+            for (int i = 0; i < nr; i++) /* fake base reads */
+                d2d(rd[i].iov[0].iov_base, disk[rd[i].disk] + rd[i].offset_blocks * blocklen, sb,
+                    st);
+            HIPOK(draid_ec_ctx_flush(ctx));
+            HIPOK(draid_ec_ctx_synchronize(ctx));
+            for (int d = 0; d < n; d++) {
+                HIPOK(draid_ec_memcpy_async(hc, chunk[d], sb, 1, st));
+                HIPOK(draid_ec_ctx_synchronize(ctx));
+                CHECK(cmp_host(hc, hd[d] + s * sb, sb));
+            }
+        }
+    /* more failures than the level tolerates */
+    r.degraded_mask = (1u << (m + 1)) - 1;
+    struct draid_base_io rd[DRAID_RAID_MAX_BASE];
+    int nr;
+    CHECK(draid_raid_stripe_degraded_read(&r, ctx, 0, (void *const *)chunk, rd, &nr) == -EIO);
+
+    for (int d = 0; d < n; d++) {
+        draid_ec_device_free(disk[d]);
+        draid_ec_device_free(chunk[d]);
+        free(hd[d]);
+    }
+    draid_ec_device_free(user);
+    draid_ec_device_free(pbuf[0]);
+    draid_ec_device_free(pbuf[1]);
+    draid_ec_device_free(junk);
+    free(hu);
+    free(hj);
+    free(ref);
+    free(hc);
+    draid_ec_ctx_destroy(ctx);
+    printf("  raid%d n=%d blocklen=%u strip=%uKiB: %s\n", lvl, n, blocklen, strip_kb,
+           g_fail ? "FAIL" : "ok");
+}
+
+int main(int argc, char **argv)
+{
+    const int cpu_only = argc > 1 && strcmp(argv[1], "--cpu-only") == 0;
+    test_geometry();
+    test_mapping();
+    printf("host logic: %s\n", g_fail ? "FAIL" : "ok");
+    if (!cpu_only) {
+        const int cfg[][4] = {{5, 3, 512, 4},  {5, 4, 4096, 4},  {5, 5, 512, 64}, {5, 5, 4096, 64},
+                              {6, 4, 512, 4},  {6, 6, 4096, 64}, {6, 10, 4096, 64}, {6, 18, 4096, 4}};
+        for (unsigned i = 0; i < sizeof(cfg) / sizeof(cfg[0]); i++)
+            run_array(cfg[i][0], cfg[i][1], (uint32_t)cfg[i][2], (uint32_t)cfg[i][3]);
+    }
+    printf("%s (%d failures)\n", g_fail ? "FAIL" : "PASS", g_fail);
+    return g_fail ? 1 : 0;
+}
