@@ -29,11 +29,11 @@ constexpr int kSlots = 4;
 constexpr uint64_t kMaxSegment = 1ull << 30;
 
 struct Group {
-    int op;  // 0 encode, 1 reconstruct
-    uint32_t k, m;
+    int op;  // 0 encode, 1 reconstruct, 2 read-modify-write update
+    uint32_t k, m;                  // op 2: k = 2 * touched chunks (old/new list pairs)
     std::vector<const void*> ptrs;  // [nseg][k+m]
     std::vector<uint32_t> len;      // [nseg]
-    std::vector<uint8_t> fail;      // [nseg][2] (reconstruct)
+    std::vector<uint8_t> fail;      // [nseg][2] failure pair (op 1) / [nseg][k/2] exponents (op 2)
 };
 
 struct Slot {
@@ -97,7 +97,8 @@ bool iter_seek(IovIter& it, size_t offset)
 // The walk of raid5_xor_stripe: runs of n = min over strips of the bytes left
 // in each strip's current iovec; one descriptor per run.
 int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* const* iovs,
-         const int* iovcnt, const size_t* offset, size_t len, uint8_t f0, uint8_t f1)
+         const int* iovcnt, const size_t* offset, size_t len, const uint8_t* meta,
+         uint32_t nmeta)
 {
     const uint32_t n = k + m;
     if (n > 512)
@@ -137,10 +138,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             it[j].off += run;
         }
         g.len.push_back(static_cast<uint32_t>(run));
-        if (op == 1) {
-            g.fail.push_back(f0);
-            g.fail.push_back(f1);
-        }
+        g.fail.insert(g.fail.end(), meta, meta + nmeta);
         ++c->queued_segments;
         remaining -= run;
     }
@@ -204,9 +202,12 @@ int flush_group(draid_ec_ctx* c, Group& g)
     const auto* lens = reinterpret_cast<const uint32_t*>(d + o_len);
     if (g.op == 0)
         e = draid::launch_encode_work(g.k, g.m, tab, lens, d + o_work, nwork, c->stream);
-    else
+    else if (g.op == 1)
         e = draid::launch_reconstruct_work(g.k, g.m, tab, lens, d + o_fail, d + o_work, nwork,
                                            c->stream);
+    else
+        e = draid::launch_update_work(g.m, g.k / 2, tab, d + o_fail, lens, d + o_work, nwork,
+                                      c->stream);
     if (e != hipSuccess)
         return ctx_fail(e, "launch (segment work list)");
     if ((e = hipEventRecord(sl.done, c->stream)) != hipSuccess)
@@ -271,7 +272,7 @@ int draid_ec_ctx_encode_sg(draid_ec_ctx* c, uint32_t k, uint32_t m,
 {
     if (!c || k < 1 || k > 255 || m < 1 || m > 2)
         return ctx_arg("encode_sg needs a ctx, 1 <= k <= 255, m in {1,2}");
-    return walk(c, 0, k, m, iovs, iovcnt, offset, len, 0xff, 0xff);
+    return walk(c, 0, k, m, iovs, iovcnt, offset, len, nullptr, 0);
 }
 
 int draid_ec_ctx_reconstruct_sg(draid_ec_ctx* c, uint32_t k, uint32_t m,
@@ -289,7 +290,44 @@ int draid_ec_ctx_reconstruct_sg(draid_ec_ctx* c, uint32_t k, uint32_t m,
     }
     if (nfail == 0)
         return 0;
-    return walk(c, 1, k, m, iovs, iovcnt, offset, len, f[0], f[1]);
+    return walk(c, 1, k, m, iovs, iovcnt, offset, len, f, 2);
+}
+
+int draid_ec_ctx_update_sg(draid_ec_ctx* c, uint32_t k, uint32_t m, uint32_t nd,
+                           const int* data_idx, const struct iovec* const* old_iovs,
+                           const int* old_cnt, const struct iovec* const* new_iovs,
+                           const int* new_cnt, const struct iovec* const* par_iovs,
+                           const int* par_cnt, size_t len)
+{
+    if (!c || k < 1 || k > 255 || m < 1 || m > 2 || nd < 1 || nd > k || !data_idx || !old_iovs ||
+        !old_cnt || !new_iovs || !new_cnt || !par_iovs || !par_cnt)
+        return ctx_arg("update_sg needs a ctx, 1 <= nd <= k <= 255, m in {1,2}, all lists");
+    // Sort the touched chunks by data index, descending (Horner with gaps).
+    uint32_t order[256];
+    for (uint32_t i = 0; i < nd; ++i) {
+        if (data_idx[i] < 0 || data_idx[i] >= static_cast<int>(k))
+            return ctx_arg("update_sg: data index out of range");
+        order[i] = i;
+    }
+    std::sort(order, order + nd, [&](uint32_t a, uint32_t b) { return data_idx[a] > data_idx[b]; });
+    const struct iovec* lists[2 * 255 + 2];
+    int cnts[2 * 255 + 2];
+    uint8_t exps[255];
+    for (uint32_t t = 0; t < nd; ++t) {
+        const uint32_t i = order[t];
+        if (t && data_idx[order[t - 1]] == data_idx[i])
+            return ctx_arg("update_sg: duplicate data index");
+        lists[2 * t] = old_iovs[i];
+        cnts[2 * t] = old_cnt[i];
+        lists[2 * t + 1] = new_iovs[i];
+        cnts[2 * t + 1] = new_cnt[i];
+        exps[t] = static_cast<uint8_t>(data_idx[i]);
+    }
+    for (uint32_t j = 0; j < m; ++j) {
+        lists[2 * nd + j] = par_iovs[j];
+        cnts[2 * nd + j] = par_cnt[j];
+    }
+    return walk(c, 2, 2 * nd, m, lists, cnts, nullptr, len, exps, nd);
 }
 
 int draid_ec_ctx_flush(draid_ec_ctx* c)

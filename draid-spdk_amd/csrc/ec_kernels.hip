@@ -578,6 +578,77 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct_work(TablePtrs pp, uint
     }
 }
 
+// ------------------------------------------------------------ read-modify-write
+
+// Small-write parity update (raid5_stripe_write_preread_complete_rmw,
+// raid5.c:705-741, extended to Q): for the nd data chunks a segment touches,
+// with old contents O_i and new contents N_i at data index e_i,
+//   P' = P ^ XOR_i (O_i ^ N_i),   Q' = Q ^ XOR_i 2^{e_i} (O_i ^ N_i).
+// The Q sum is a Horner evaluation with gaps over the exponents, sorted
+// descending by the host: q = mul2^(e_prev - e_i)(q) ^ delta_i, then
+// mul2^(e_last)(q) -- at most k-1 doublings per element, no table lookups.
+// Segment table row: [O_0, N_0, O_1, N_1, ..., P, (Q)]; exps row: e_0 > e_1 > ...
+template <int M, class C>
+__global__ __launch_bounds__(C::NTHR) void k_update_work(const uint8_t* const* tab, uint32_t nd,
+                                                         const uint8_t* exps,
+                                                         const uint32_t* seg_len,
+                                                         const WorkItem* work, uint32_t nwork)
+{
+    constexpr uint32_t EPB = static_cast<uint32_t>(C::NTHR) * C::U;
+    const uint32_t stride = 2 * nd + M;
+    for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
+        const WorkItem w = work[b];
+        const uint32_t len = seg_len[w.seg];
+        const uint8_t* const* row = tab + (size_t)w.seg * stride;
+        const uint8_t* ex = exps + (size_t)w.seg * nd;
+        const uint8_t* pP = row[2 * nd];
+        const uint8_t* pQ = M == 2 ? row[2 * nd + 1] : pP;
+        uintptr_t acc = 0;
+        for (uint32_t t = 0; t < stride; ++t)
+            acc |= reinterpret_cast<uintptr_t>(row[t]);
+        auto body = [&](auto tag, uint32_t i) {
+            using W = decltype(tag);
+            using MW = Mem<W>;
+            W dp = W(0), dq = W(0);
+            int prev = -1;
+            for (uint32_t t = 0; t < nd; ++t) {
+                const W delta = MW::template ld<true>(row[2 * t], i) ^
+                                MW::template ld<true>(row[2 * t + 1], i);
+                dp ^= delta;
+                if constexpr (M == 2) {
+                    const int e = ex[t];
+                    for (int g = (prev < 0 ? 0 : prev - e); g > 0; --g)
+                        dq = gf_mul2(dq);
+                    dq ^= delta;
+                    prev = e;
+                }
+            }
+            MW::template st<true>(pP, i, MW::template ld<true>(pP, i) ^ dp);
+            if constexpr (M == 2) {
+                for (int g = prev; g > 0; --g)
+                    dq = gf_mul2(dq);
+                MW::template st<true>(pQ, i, MW::template ld<true>(pQ, i) ^ dq);
+            }
+        };
+        if ((acc & 15u) == 0) {
+            const uint32_t nvec = len >> 4;
+            for (uint32_t u = 0; u < C::U; ++u) {
+                const uint32_t i = w.chunk * EPB + u * C::NTHR + threadIdx.x;
+                if (i < nvec)
+                    body(u32x4{}, i);
+            }
+            const uint32_t tail = len & 15u;
+            const uint32_t cps = (len + EPB * 16 - 1) / (EPB * 16);
+            if (tail && w.chunk == cps - 1 && threadIdx.x < tail)
+                body(uint32_t{}, nvec * 16 + threadIdx.x);
+        } else {
+            const uint32_t b1 = min(len, (w.chunk + 1) * EPB * 16);
+            for (uint32_t i = w.chunk * EPB * 16 + threadIdx.x; i < b1; i += C::NTHR)
+                body(uint32_t{}, i);
+        }
+    }
+}
+
 // ------------------------------------------------------------ gf_vect_mul
 
 __global__ __launch_bounds__(kThreads) void k_gf_vect_mul(const uint8_t* src, uint8_t* dst,
@@ -849,6 +920,8 @@ static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t k,
 
 uint32_t work_chunk_bytes(int op, uint32_t k)
 {
+    if (op == 2)
+        return 256u * 1u * 16u;  // update: CfgDefault<1>
     int u = 2;
     switch (k) {
 #define DRAID_CASE(K)                                       \
@@ -900,6 +973,22 @@ hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const*
                    ? go_reconstruct_work<0, 1, CfgDefault<2>>(table, k, seg_len, fail, work, nwork, st)
                    : go_reconstruct_work<0, 2, CfgDefault<2>>(table, k, seg_len, fail, work, nwork, st);
     }
+}
+
+hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* table,
+                              const uint8_t* exps, const uint32_t* seg_len, const void* work,
+                              uint32_t nwork, hipStream_t st)
+{
+    using C = CfgDefault<1>;
+    if (nwork == 0)
+        return hipSuccess;
+    if (m == 1)
+        hipLaunchKernelGGL((k_update_work<1, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
+                           exps, seg_len, static_cast<const WorkItem*>(work), nwork);
+    else
+        hipLaunchKernelGGL((k_update_work<2, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
+                           exps, seg_len, static_cast<const WorkItem*>(work), nwork);
+    return hipGetLastError();
 }
 
 hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,

@@ -38,7 +38,8 @@ hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len,
 hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,
                               uint8_t* dst, hipStream_t stream);
 
-// Segment work lists (scatter-gather, ec_ctx.cpp).  op: 0 encode, 1 reconstruct.
+// Segment work lists (scatter-gather, ec_ctx.cpp).  op: 0 encode, 1 reconstruct,
+// 2 read-modify-write update.
 // A work item is {segment, chunk}; chunk covers work_chunk_bytes(op, k) bytes.
 uint32_t work_chunk_bytes(int op, uint32_t k);
 hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,
@@ -47,6 +48,12 @@ hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* tabl
 hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
                                    const uint32_t* seg_len, const uint8_t* fail, const void* work,
                                    uint32_t nwork, hipStream_t stream);
+
+// Read-modify-write parity update over a segment work list (op 2): table rows
+// [O_0, N_0, ..., O_{nd-1}, N_{nd-1}, P, (Q)], exps rows sorted descending.
+hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* table,
+                              const uint8_t* exps, const uint32_t* seg_len, const void* work,
+                              uint32_t nwork, hipStream_t stream);
 
 // Error reporting shared by every C entry point (ec_api.cpp): records the
 // message for draid_ec_last_error(); fail_hip returns -hipError, fail_arg 1.

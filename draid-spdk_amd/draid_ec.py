@@ -30,6 +30,7 @@ EXPORTS = (
     "draid_ec_ctx_stream", "draid_ec_ctx_encode_sg", "draid_ec_ctx_reconstruct_sg",
     "draid_ec_ctx_flush", "draid_ec_ctx_query", "draid_ec_ctx_synchronize",
     "draid_ec_ctx_queued", "draid_ec_host_encode", "draid_ec_host_reconstruct",
+    "draid_ec_ctx_update_sg",
 )
 
 
@@ -110,6 +111,8 @@ def lib() -> C.CDLL:
         L.draid_ec_ctx_encode_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t]
         L.draid_ec_ctx_reconstruct_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp,
                                                   C.c_size_t, i32, vp]
+        L.draid_ec_ctx_update_sg.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp,
+                                             vp, vp, vp, vp, C.c_size_t]
         L.draid_ec_host_encode.argtypes = [C.POINTER(HostStripes), C.c_uint32]
         L.draid_ec_host_reconstruct.argtypes = [C.POINTER(HostStripes), vp, C.c_uint32]
         _lib = L
@@ -264,6 +267,15 @@ class Ctx:
         f = (C.c_int * max(1, len(fail)))(*fail)
         return _check(lib().draid_ec_ctx_reconstruct_sg(self.h, k, m, heads, cnts, off, length,
                                                         len(fail), f), "ctx_reconstruct_sg")
+
+    def update_sg(self, k, m, data_idx, old, new, parity, length):
+        """old/new: per touched chunk lists of (ptr, len) runs; parity: [P runs, (Q runs)]."""
+        oa, oh, oc = self._lists(old)
+        na, nh, nc = self._lists(new)
+        pa, ph, pc = self._lists(parity)
+        idx = (C.c_int * len(data_idx))(*data_idx)
+        return _check(lib().draid_ec_ctx_update_sg(self.h, k, m, len(data_idx), idx, oh, oc, nh,
+                                                   nc, ph, pc, length), "ctx_update_sg")
 
     def flush(self):
         return _check(lib().draid_ec_ctx_flush(self.h), "ctx_flush")

@@ -141,6 +141,18 @@ int draid_ec_ctx_reconstruct_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m,
                                 const struct iovec *const *iovs, const int *iovcnt,
                                 const size_t *offset, size_t len, int nfail, const int *fail);
 
+/* Queue a read-modify-write parity update (raid5_stripe_write_preread_complete_rmw,
+ * raid5.c:705-741, extended to Q): nd touched data chunks with distinct data
+ * indices data_idx[i] < k, each with iovec lists of its old and new contents;
+ * par_iovs[0] is P and (m == 2) par_iovs[1] is Q, updated in place:
+ *   P ^= XOR_i (old_i ^ new_i),  Q ^= XOR_i 2^{data_idx[i]} (old_i ^ new_i).
+ * Every list covers `len` bytes from its start. */
+int draid_ec_ctx_update_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m, uint32_t nd,
+                           const int *data_idx, const struct iovec *const *old_iovs,
+                           const int *old_cnt, const struct iovec *const *new_iovs,
+                           const int *new_cnt, const struct iovec *const *par_iovs,
+                           const int *par_cnt, size_t len);
+
 /* Launch everything queued (non-blocking; blocks only if the descriptor ring
  * is 4 flushes behind).  draid_ec_ctx_query: 0 idle, 1 running, < 0 error. */
 int draid_ec_ctx_flush(draid_ec_ctx *ctx);

@@ -1,0 +1,74 @@
+"""GPU tests of the read-modify-write parity update (draid_ec_ctx_update_sg):
+after P ^= sum(delta), Q ^= sum(2^i delta) the parity must equal a full
+re-encode of the updated stripe by the oracle (raid5.c:705-741 semantics,
+extended to Q)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _runs(rng, base, length, pieces):
+    """Split [base, base+length) into up to `pieces` contiguous runs."""
+    if pieces <= 1 or length < 2:
+        return [(base, length)]
+    cuts = sorted(rng.choice(np.arange(1, length), size=min(pieces - 1, length - 1),
+                             replace=False).tolist())
+    b = [0] + cuts + [length]
+    return [(base + x, y - x) for x, y in zip(b, b[1:])]
+
+
+@pytest.mark.parametrize("k,m,L,B", [(4, 1, 4096, 6), (8, 2, 65536, 5), (16, 2, 8192, 4),
+                                     (8, 2, 1000, 5)])
+def test_rmw_update_matches_reencode(ec, k, m, L, B):
+    rng = np.random.default_rng(k * 100 + L)
+    n = k + m
+    host = np.zeros((B, n, L), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    assert oracle.encode_strided(host.reshape(-1), k, m, L, B, L, n * L) == 0
+    stripes = torch.from_numpy(host.copy()).to(DEV)
+    newdata = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).to(DEV)
+    olddata = stripes[:, :k].clone()           # the RMW preread of the touched chunks
+    expect = host.copy()
+    ctx = ec.Ctx()
+    try:
+        for s in range(B):
+            nd = int(rng.integers(1, k + 1))
+            idx = sorted(rng.choice(k, nd, replace=False).tolist(), key=lambda _: rng.random())
+            a = int(rng.integers(0, L // 2))
+            b = int(rng.integers(a + 1, L + 1))
+            ln = b - a
+            pc = int(rng.integers(1, 4))
+            old = [_runs(rng, olddata[s, i].data_ptr() + a, ln, pc) for i in idx]
+            new = [_runs(rng, newdata[s, i].data_ptr() + a, ln, pc) for i in idx]
+            par = [_runs(rng, stripes[s, k + j].data_ptr() + a, ln, pc) for j in range(m)]
+            assert ctx.update_sg(k, m, idx, old, new, par, ln) == 0
+            for i in idx:
+                expect[s, i, a:b] = newdata[s, i, a:b].cpu().numpy()
+        ctx.flush()
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    ref = expect.copy()
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, B, L, n * L) == 0
+    got = stripes.cpu().numpy()
+    assert (got[:, k:] == ref[:, k:]).all()
+    assert (got[:, :k] == host[:, :k]).all()      # update touches parity only
+
+
+def test_rmw_rejects_bad_indices(ec):
+    ctx = ec.Ctx()
+    try:
+        t = torch.zeros(1 << 16, dtype=torch.uint8, device=DEV)
+        p = t.data_ptr()
+        one = [[(p, 4096)]]
+        assert ctx.update_sg(4, 1, [4], one, one, one, 4096) == 1          # index >= k
+        assert ctx.update_sg(4, 1, [1, 1], one * 2, one * 2, one, 4096) == 1  # duplicate
+        ctx.flush()
+        ctx.synchronize()
+    finally:
+        ctx.close()
