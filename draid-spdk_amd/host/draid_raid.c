@@ -226,3 +226,220 @@ int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ct
                                          nfail, fail);
     return rc > 0 ? -EINVAL : rc;
 }
+
+/* ------------------------------------------------------------ partial writes */
+
+static void add_io(struct draid_base_io *io, int disk, uint64_t stripe_lba, uint64_t off,
+                   uint64_t blocks, void *buf, uint32_t blocklen)
+{
+    io->disk = disk;
+    io->offset_blocks = stripe_lba + off;
+    io->num_blocks = blocks;
+    io->iovcnt = 1;
+    io->iov[0].iov_base = (uint8_t *)buf + off * blocklen;
+    io->iov[0].iov_len = blocks * blocklen;
+}
+
+/* raid5_stripe_write, raid5.c:779-867 */
+int draid_raid_plan_write(const struct draid_raid *r, const struct draid_stripe_req *req,
+                          struct draid_write_plan *plan, void *const *preread_buf,
+                          struct draid_base_io *reads, int *nreads)
+{
+    if (!r || !req || !plan || !preread_buf || !reads || !nreads || req->full_stripe)
+        return -EINVAL;
+    const int n = r->num_base_bdevs;
+    const uint64_t strip = r->strip_size, lba = req->stripe_index << r->strip_size_shift;
+    memset(plan, 0, sizeof(*plan));
+    if (req->first_data == req->last_data) {
+        const int fd = draid_raid_data_disk(r, req->stripe_index, req->first_data);
+        plan->p_offset = req->chunk[fd].req_offset;
+        plan->p_blocks = req->chunk[fd].req_blocks;
+    } else {
+        plan->p_offset = 0;
+        plan->p_blocks = strip;
+    }
+    int balance = 0;
+    for (int disk = 0; disk < n; disk++) {
+        if (disk == req->p_disk || disk == req->q_disk)
+            continue;
+        if (req->chunk[disk].req_blocks < plan->p_blocks)
+            balance++;
+        if (req->chunk[disk].req_blocks > 0)
+            balance--;
+    }
+    plan->mode = balance > 0 ? DRAID_WRITE_RMW : DRAID_WRITE_RCW;
+    int nr = 0;
+    for (int disk = 0; disk < n; disk++) {
+        const bool parity = disk == req->p_disk || disk == req->q_disk;
+        const struct draid_chunk_req *c = &req->chunk[disk];
+        struct draid_chunk_req *pr = &plan->preread[disk];
+        if (plan->mode == DRAID_WRITE_RMW) {
+            /* old data of the touched ranges and the old parity range */
+            pr->req_offset = parity ? plan->p_offset : c->req_offset;
+            pr->req_blocks = parity ? plan->p_blocks : c->req_blocks;
+        } else if (parity) {
+            pr->req_blocks = 0; /* reconstruct-write: parity is recomputed */
+        } else if (req->first_data == req->last_data) {
+            if (!c->req_blocks) { /* non-request chunks: the parity range */
+                pr->req_offset = plan->p_offset;
+                pr->req_blocks = plan->p_blocks;
+            }
+        } else if (c->req_offset) { /* complete the chunk in front of the request */
+            pr->req_offset = 0;
+            pr->req_blocks = c->req_offset;
+        } else { /* behind the request (the whole chunk if untouched) */
+            pr->req_offset = c->req_blocks;
+            pr->req_blocks = strip - c->req_blocks;
+        }
+        if (pr->req_blocks)
+            add_io(&reads[nr++], disk, lba, pr->req_offset, pr->req_blocks, preread_buf[disk],
+                   r->blocklen);
+    }
+    *nreads = nr;
+    return 0;
+}
+
+/* User-iovec slice holding data chunk d's strip blocks [a, b). */
+static int user_slice(const struct draid_raid *r, const struct draid_stripe_req *req, int d,
+                      uint64_t a, uint64_t b, const struct iovec *iov, int iovcnt,
+                      struct iovec *out, int out_max)
+{
+    const uint64_t from = (uint64_t)req->first_data * r->strip_size +
+                          req->chunk[draid_raid_data_disk(r, req->stripe_index,
+                                                          req->first_data)].req_offset;
+    const uint64_t soff = (uint64_t)d * r->strip_size + a; /* stripe offset of block a */
+    return draid_raid_map_iov(out, out_max, iov, iovcnt, (soff - from) * r->blocklen,
+                              (b - a) * r->blocklen);
+}
+
+int draid_raid_stripe_write_partial(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                    const struct draid_stripe_req *req,
+                                    const struct draid_write_plan *plan, const struct iovec *iov,
+                                    int iovcnt, void *const *preread_buf,
+                                    struct draid_base_io *writes, int *nwrites)
+{
+    if (!r || !ctx || !req || !plan || !iov || !preread_buf || !writes || !nwrites)
+        return -EINVAL;
+    const int n = r->num_base_bdevs, m = r->max_degraded, k = n - m;
+    const uint32_t bl = r->blocklen;
+    const uint64_t lba = req->stripe_index << r->strip_size_shift;
+    const uint64_t p0 = plan->p_offset, p1 = plan->p_offset + plan->p_blocks;
+    int pdisk[2] = {req->p_disk, req->q_disk};
+    struct iovec pv[2];
+    const struct iovec *plist[2] = {&pv[0], &pv[1]};
+    int pcnt[2] = {1, 1};
+    int rc = 0;
+
+    if (plan->mode == DRAID_WRITE_RMW) {
+        /* elementary strip ranges between every touched chunk's boundaries */
+        uint64_t cut[2 * DRAID_RAID_MAX_BASE + 2];
+        int nc = 0;
+        for (int d = req->first_data; d <= req->last_data; d++) {
+            const struct draid_chunk_req *c =
+                &req->chunk[draid_raid_data_disk(r, req->stripe_index, d)];
+            cut[nc++] = c->req_offset;
+            cut[nc++] = c->req_offset + c->req_blocks;
+        }
+        for (int i = 1; i < nc; i++) /* insertion sort: nc <= 2k */
+            for (int j = i; j > 0 && cut[j - 1] > cut[j]; j--) {
+                uint64_t t = cut[j];
+                cut[j] = cut[j - 1];
+                cut[j - 1] = t;
+            }
+        static __thread struct iovec ov[DRAID_RAID_MAX_BASE], nv[DRAID_RAID_MAX_BASE]
+                                                                 [DRAID_RAID_MAX_IOV];
+        for (int i = 0; i + 1 < nc; i++) {
+            const uint64_t a = cut[i], b = cut[i + 1];
+            if (a == b)
+                continue;
+            int idx[DRAID_RAID_MAX_BASE], nd = 0, ncnt[DRAID_RAID_MAX_BASE], ocnt[DRAID_RAID_MAX_BASE];
+            const struct iovec *ol[DRAID_RAID_MAX_BASE], *nl[DRAID_RAID_MAX_BASE];
+            for (int d = req->first_data; d <= req->last_data; d++) {
+                const int disk = draid_raid_data_disk(r, req->stripe_index, d);
+                const struct draid_chunk_req *c = &req->chunk[disk];
+                if (c->req_offset > a || c->req_offset + c->req_blocks < b)
+                    continue;
+                ov[nd].iov_base = (uint8_t *)preread_buf[disk] + a * bl;
+                ov[nd].iov_len = (b - a) * bl;
+                ol[nd] = &ov[nd];
+                ocnt[nd] = 1;
+                int cnt = user_slice(r, req, d, a, b, iov, iovcnt, nv[nd], DRAID_RAID_MAX_IOV);
+                if (cnt < 0)
+                    return cnt;
+                nl[nd] = nv[nd];
+                ncnt[nd] = cnt;
+                idx[nd++] = d;
+            }
+            if (!nd)
+                continue;
+            for (int j = 0; j < m; j++) {
+                pv[j].iov_base = (uint8_t *)preread_buf[pdisk[j]] + a * bl;
+                pv[j].iov_len = (b - a) * bl;
+            }
+            rc = draid_ec_ctx_update_sg(ctx, (uint32_t)k, (uint32_t)m, (uint32_t)nd, idx, ol, ocnt,
+                                        nl, ncnt, plist, pcnt, (b - a) * bl);
+            if (rc)
+                return rc > 0 ? -EINVAL : rc;
+        }
+    } else {
+        /* reconstruct-write: every data chunk over [p0, p1) from preread + new data */
+        static __thread struct iovec dv[DRAID_RAID_MAX_BASE][DRAID_RAID_MAX_IOV + 2];
+        const struct iovec *dl[DRAID_RAID_MAX_BASE + 2];
+        int dcnt[DRAID_RAID_MAX_BASE + 2];
+        for (int d = 0; d < k; d++) {
+            const int disk = draid_raid_data_disk(r, req->stripe_index, d);
+            const struct draid_chunk_req *c = &req->chunk[disk];
+            int cnt = 0;
+            const uint64_t u0 = c->req_blocks ? c->req_offset : p1;
+            const uint64_t u1 = c->req_blocks ? c->req_offset + c->req_blocks : p1;
+            if (p0 < u0) { /* preread in front */
+                dv[d][cnt].iov_base = (uint8_t *)preread_buf[disk] + p0 * bl;
+                dv[d][cnt++].iov_len = (u0 - p0) * bl;
+            }
+            if (u1 > u0) {
+                int c2 = user_slice(r, req, d, u0, u1, iov, iovcnt, &dv[d][cnt],
+                                    DRAID_RAID_MAX_IOV);
+                if (c2 < 0)
+                    return c2;
+                cnt += c2;
+            }
+            if (u1 < p1) { /* preread behind */
+                dv[d][cnt].iov_base = (uint8_t *)preread_buf[disk] + u1 * bl;
+                dv[d][cnt++].iov_len = (p1 - u1) * bl;
+            }
+            dl[d] = dv[d];
+            dcnt[d] = cnt;
+        }
+        for (int j = 0; j < m; j++) {
+            pv[j].iov_base = (uint8_t *)preread_buf[pdisk[j]] + p0 * bl;
+            pv[j].iov_len = (p1 - p0) * bl;
+            dl[k + j] = &pv[j];
+            dcnt[k + j] = 1;
+        }
+        rc = draid_ec_ctx_encode_sg(ctx, (uint32_t)k, (uint32_t)m, dl, dcnt, NULL, (p1 - p0) * bl);
+        if (rc)
+            return rc > 0 ? -EINVAL : rc;
+    }
+
+    /* base writes: the new data ranges, then the parity range */
+    int nw = 0;
+    for (int d = req->first_data; d <= req->last_data; d++) {
+        const int disk = draid_raid_data_disk(r, req->stripe_index, d);
+        const struct draid_chunk_req *c = &req->chunk[disk];
+        if (!c->req_blocks)
+            continue;
+        struct draid_base_io *w = &writes[nw++];
+        w->disk = disk;
+        w->offset_blocks = lba + c->req_offset;
+        w->num_blocks = c->req_blocks;
+        int cnt = user_slice(r, req, d, c->req_offset, c->req_offset + c->req_blocks, iov, iovcnt,
+                             w->iov, DRAID_RAID_MAX_IOV);
+        if (cnt < 0)
+            return cnt;
+        w->iovcnt = cnt;
+    }
+    for (int j = 0; j < m; j++)
+        add_io(&writes[nw++], pdisk[j], lba, p0, p1 - p0, preread_buf[pdisk[j]], bl);
+    *nwrites = nw;
+    return 0;
+}

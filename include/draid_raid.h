@@ -98,6 +98,37 @@ int draid_raid_stripe_write(const struct draid_raid *r, draid_ec_ctx *ctx,
                             int iovcnt, void *const parity_buf[2],
                             struct draid_base_io *writes, int *nwrites);
 
+/* Partial-stripe writes, two phases as in raid5_stripe_write (raid5.c:779-867).
+ * The vote: with the parity range = the touched chunk's range (one chunk) or the
+ * whole strip (several), every data chunk with fewer requested blocks than the
+ * parity range votes for read-modify-write, every touched chunk against. */
+enum draid_write_mode { DRAID_WRITE_RMW = 1, DRAID_WRITE_RCW = 2 };
+
+struct draid_write_plan {
+    int mode;
+    uint64_t p_offset, p_blocks;                         /* parity range within the strip */
+    struct draid_chunk_req preread[DRAID_RAID_MAX_BASE]; /* per disk; blocks == 0: none */
+};
+
+/* Phase 1: vote and list the prereads.  preread_buf[disk] are strip-sized
+ * buffers; a preread of [off, off+blocks) lands at the same offset in them.
+ * For P and Q they also receive the new parity range.  Full-stripe requests
+ * need no plan (draid_raid_stripe_write). */
+int draid_raid_plan_write(const struct draid_raid *r, const struct draid_stripe_req *req,
+                          struct draid_write_plan *plan, void *const *preread_buf,
+                          struct draid_base_io *reads, int *nreads);
+
+/* Phase 2, once the prereads are in (raid5_stripe_write_preread_complete[_rmw],
+ * raid5.c:705-777): queue the parity work on ctx -- RMW: P ^= old ^ new (and
+ * Q ^= 2^i (old ^ new)) per touched chunk range; RCW: P (and Q) re-encoded over
+ * the parity range from preread and new data -- into preread_buf[p] (and [q]),
+ * and fill writes[] with the new data ranges and the parity range. */
+int draid_raid_stripe_write_partial(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                    const struct draid_stripe_req *req,
+                                    const struct draid_write_plan *plan, const struct iovec *iov,
+                                    int iovcnt, void *const *preread_buf,
+                                    struct draid_base_io *writes, int *nwrites);
+
 /* Degraded read of a whole stripe (raid5_stripe_read + the reconstruct of
  * raid5_complete_reconstructed_stripe_request, raid5.c:544-594,869-946,
  * generalised to two failures): `chunk_buf[disk]` are the stripe's per-disk

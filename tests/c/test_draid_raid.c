@@ -219,6 +219,57 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
         CHECK(draid_raid_stripe_write(&r, ctx, &pr, iov, 3, pq, w, &nw) == -EINVAL);
     }
 
+    /* partial-stripe writes: the RMW / RCW vote, prereads, parity update, writes */
+    uint8_t *pre[DRAID_RAID_MAX_BASE], *nub;
+    for (int d = 0; d < n; d++)
+        HIPOK(draid_ec_device_alloc((void **)&pre[d], sb));
+    HIPOK(draid_ec_device_alloc((void **)&nub, ub));
+    uint8_t *hn = malloc(ub);
+    uint64_t rng = 0x9e3779b97f4a7c15ull ^ (uint64_t)(n * 131 + lvl);
+    int modes[3] = {0, 0, 0};
+    for (int t = 0; t < 24; t++) {
+        const uint64_t s = orc_splitmix64(&rng) % r.total_stripes;
+        const uint64_t off = orc_splitmix64(&rng) % r.stripe_blocks;
+        uint64_t len = 1 + orc_splitmix64(&rng) % (r.stripe_blocks - off);
+        if (t % 4 == 0) /* some single-chunk requests */
+            len = 1 + (orc_splitmix64(&rng) % (strip - off % strip));
+        if (off == 0 && len == r.stripe_blocks)
+            continue;
+        orc_fill_splitmix(hn, len * blocklen, orc_splitmix64(&rng));
+        HIPOK(draid_ec_memcpy_async(nub, hn, len * blocklen, 0, st));
+        struct draid_stripe_req q;
+        CHECK(draid_raid_map_request(&r, s * r.stripe_blocks + off, len, &q) == 0);
+        CHECK(!q.full_stripe);
+        struct draid_write_plan plan;
+        struct draid_base_io io[2 * DRAID_RAID_MAX_BASE];
+        int nio = 0;
+        CHECK(draid_raid_plan_write(&r, &q, &plan, (void *const *)pre, io, &nio) == 0);
+        modes[plan.mode]++;
+        for (int i = 0; i < nio; i++) /* fake base prereads */
+            d2d(io[i].iov[0].iov_base, disk[io[i].disk] + io[i].offset_blocks * blocklen,
+                io[i].num_blocks * blocklen, st);
+        const size_t half = (len * blocklen) / 2;
+        struct iovec uiov[2] = {{nub, half}, {nub + half, len * blocklen - half}};
+        CHECK(draid_raid_stripe_write_partial(&r, ctx, &q, &plan, uiov, 2, (void *const *)pre, io,
+                                              &nio) == 0);
+        HIPOK(draid_ec_ctx_flush(ctx));
+        for (int i = 0; i < nio; i++) { /* fake base writes (stream-ordered after the kernel) */
+            size_t o = (size_t)io[i].offset_blocks * blocklen;
+            for (int v = 0; v < io[i].iovcnt; v++) {
+                d2d(disk[io[i].disk] + o, io[i].iov[v].iov_base, io[i].iov[v].iov_len, st);
+                o += io[i].iov[v].iov_len;
+            }
+        }
+        HIPOK(draid_ec_ctx_synchronize(ctx));
+        memcpy(hu + s * ub + off * blocklen, hn, len * blocklen);
+    }
+    if (k >= 3)
+        CHECK(modes[DRAID_WRITE_RMW] > 0 && modes[DRAID_WRITE_RCW] > 0);
+    for (int d = 0; d < n; d++)
+        draid_ec_device_free(pre[d]);
+    draid_ec_device_free(nub);
+    free(hn);
+
     /* every stripe on the fake disks: data in place, parity == oracle */
     uint8_t *hd[DRAID_RAID_MAX_BASE];
     for (int d = 0; d < n; d++) {
@@ -289,7 +340,8 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
     free(ref);
     free(hc);
     draid_ec_ctx_destroy(ctx);
-    printf("  raid%d n=%d blocklen=%u strip=%uKiB: %s\n", lvl, n, blocklen, strip_kb,
+    printf("  raid%d n=%d blocklen=%u strip=%uKiB (partial writes rmw=%d rcw=%d): %s\n", lvl, n,
+           blocklen, strip_kb, modes[DRAID_WRITE_RMW], modes[DRAID_WRITE_RCW],
            g_fail ? "FAIL" : "ok");
 }
 
