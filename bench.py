@@ -140,6 +140,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="backend of the timing collectives (nccl = RCCL; gloo only for "
+                         "rehearsing several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -149,9 +152,15 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # One rank per GPU; with fewer visible GPUs than ranks (a rehearsal on a
+    # single-GPU box) ranks share devices round-robin.
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     ec.lib()
@@ -206,7 +215,8 @@ def main() -> None:
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     rec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     units = 2.0 * k * S * B * args.steps  # user-data bytes through both passes
-    elapsed, units = reduce_timing(elapsed, units, dev)
+    elapsed, units = reduce_timing(elapsed, units,
+                                   dev if args.dist_backend == "nccl" else torch.device("cpu"))
 
     verified = None
     if not args.no_verify:

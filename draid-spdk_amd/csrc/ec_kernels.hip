@@ -337,7 +337,7 @@ __device__ __forceinline__ void plan_constants(RecPlan& pl, const uint8_t* t_exp
 // Loads and syndrome accumulation for U elements, then `constants(pl)` (which
 // may stage tables and hit a workgroup barrier -- every lane calls it exactly
 // once, after its loads are in flight), then the outputs.
-template <int KT, int M, int U, int POL, bool BOUNDED, class W, class Ptrs, class F>
+template <int KT, int M, int U, int POL, bool BOUNDED, bool NOMUL, class W, class Ptrs, class F>
 __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k, RecPlan& pl,
                                               uint32_t i0, uint32_t stride, uint32_t n,
                                               F&& constants)
@@ -403,7 +403,8 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
         } else {
             const W pxy = pv[u] ^ ps[u];
             const W qxy = qv[u] ^ qs[u];
-            const W dx = gf_mulc(pl.t1, pxy) ^ gf_mulc(pl.t2, qxy);
+            // NOMUL: diagnostic builds only (tools/sweep.py) -- wrong results.
+            const W dx = NOMUL ? (pxy ^ qxy) : (gf_mulc(pl.t1, pxy) ^ gf_mulc(pl.t2, qxy));
             MW::template st<(POL & 2) != 0>(pX, i, dx);
             MW::template st<(POL & 2) != 0>(pY, i, pxy ^ dx);
         }
@@ -436,25 +437,26 @@ __device__ __forceinline__ void reconstruct_item(const Ptrs& pp, uint32_t s, uin
     if (stripe_aligned<KT, M>(pp, s, k)) {
         const uint32_t i0 = c * EPB + threadIdx.x;
         if ((c + 1) * EPB <= nvec) {
-            recover_elems<KT, M, U, POL, false, u32x4>(pp, s, k, pl, i0, NTHR, nvec, constants);
+            recover_elems<KT, M, U, POL, false, C::PLAN == 3, u32x4>(pp, s, k, pl, i0, NTHR, nvec,
+                                                                      constants);
         } else {
             // Partial last chunk (rare): one vector at a time keeps this path's
             // registers below the main path's, so it does not cap occupancy.
             constants(pl);
 #pragma unroll 1
             for (int u = 0; u < U; ++u)
-                recover_elems<KT, M, 1, POL, true, u32x4>(pp, s, k, pl, i0 + u * NTHR, NTHR, nvec,
+                recover_elems<KT, M, 1, POL, true, false, u32x4>(pp, s, k, pl, i0 + u * NTHR, NTHR, nvec,
                                                           none);
         }
         const uint32_t tail = len & 15u;
         if (tail && c == cps - 1 && threadIdx.x < tail)
-            recover_elems<0, M, 1, 0, true, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
+            recover_elems<0, M, 1, 0, true, false, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
                                                       NTHR, len, none);
     } else {
         constants(pl);
         const uint32_t b1 = min(len, (c + 1) * EPB * 16);
         for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += NTHR)
-            recover_elems<0, M, 1, 0, true, uint32_t>(pp, s, k, pl, b, NTHR, b1, none);
+            recover_elems<0, M, 1, 0, true, false, uint32_t>(pp, s, k, pl, b, NTHR, b1, none);
     }
 }
 
@@ -496,7 +498,7 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
         RecPlan pl = decode_failures<M>(k, f0, f1);
         if (pl.skip)
             continue;  // uniform across the workgroup
-        if constexpr (C::PLAN == 2) {
+        if constexpr (C::PLAN == 2 || C::PLAN == 3) {
             // DIAGNOSTIC ONLY (tools/sweep.py): constants left zero, no LDS, no
             // barrier -- wrong results, measures what the plan step costs.
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
@@ -799,8 +801,9 @@ using V11 = Cfg<512, 2, 3, 0, 0>;  // 512 lanes, U=2
 using V12 = Cfg<256, 4, 3, 0, 0>;  // U=4
 using V13 = Cfg<256, 2, 3, 0, 2>;  // DIAGNOSTIC: reconstruct without the plan step, U=2
 using V14 = Cfg<256, 1, 3, 0, 2>;  // DIAGNOSTIC: reconstruct without the plan step, U=1
+using V15 = Cfg<256, 1, 3, 0, 3>;  // DIAGNOSTIC: no plan step and no GF multiplies, U=1
 #define DRAID_VARIANTS(X) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5) X(6, V6) X(7, V7) X(8, V8) \
-    X(9, V9) X(10, V10) X(11, V11) X(12, V12) X(13, V13) X(14, V14)
+    X(9, V9) X(10, V10) X(11, V11) X(12, V12) X(13, V13) X(14, V14) X(15, V15)
 
 template <int K, int M>
 static hipError_t variant_encode(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
