@@ -11,8 +11,11 @@ import oracle
 import draid_ec
 
 
-def header_functions():
-    txt = open(draid_ec.HEADER).read()
+INCLUDE = os.path.dirname(draid_ec.HEADER)
+
+
+def header_functions(path):
+    txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(draid_\w+)\s*\(", txt)))
 
@@ -20,11 +23,16 @@ def header_functions():
 def test_library_exports_header_symbols():
     draid_ec.build()
     L = ctypes.CDLL(draid_ec.LIB_PATH)
-    names = header_functions()
-    assert len(names) >= 20
-    for n in names:
-        assert hasattr(L, n), f"libdraid_ec.so does not export {n}"
-    assert sorted(draid_ec.EXPORTS) == names
+    headers = [os.path.join(INCLUDE, f) for f in sorted(os.listdir(INCLUDE)) if f.endswith(".h")]
+    assert len(headers) >= 2
+    total = 0
+    for h in headers:
+        for n in header_functions(h):
+            assert hasattr(L, n), f"libdraid_ec.so does not export {n} ({h})"
+            total += 1
+    assert total >= 35
+    # the ctypes binding declares exactly the C ABI of draid_ec.h
+    assert sorted(draid_ec.EXPORTS) == header_functions(draid_ec.HEADER)
 
 
 def test_library_is_gfx950_code_object():
