@@ -270,6 +270,43 @@ int draid_ec_reconstruct(const draid_ec_stripe_batch* b, const uint8_t* fail, vo
     return e == hipSuccess ? 0 : fail_hip(e, "launch_reconstruct");
 }
 
+static int check_strided(const draid_ec_strided_stripes* d)
+{
+    if (!d)
+        return fail_arg("strided stripes descriptor is NULL");
+    if (d->k < 1 || d->k > 255 || d->m < 1 || d->m > 2 || d->flags != 0)
+        return fail_arg("strided stripes need 1 <= k <= 255, m in {1,2}, flags == 0");
+    if (d->nstripes && d->strip_len && !d->base)
+        return fail_arg("strided stripes base is NULL");
+    return 0;
+}
+
+int draid_ec_encode_strided(const draid_ec_strided_stripes* d, void* stream)
+{
+    int rc = check_strided(d);
+    if (rc || !d->nstripes || !d->strip_len)
+        return rc;
+    hipError_t e = draid::launch_encode_strided(d->k, d->m, d->strip_len, d->nstripes,
+                                                static_cast<const uint8_t*>(d->base),
+                                                d->strip_stride, d->stripe_stride,
+                                                static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail_hip(e, "launch_encode_strided");
+}
+
+int draid_ec_reconstruct_strided(const draid_ec_strided_stripes* d, const uint8_t* fail,
+                                 void* stream)
+{
+    int rc = check_strided(d);
+    if (rc || !d->nstripes || !d->strip_len)
+        return rc;
+    if (!fail)
+        return fail_arg("reconstruct: fail table is NULL");
+    hipError_t e = draid::launch_reconstruct_strided(
+        d->k, d->m, d->strip_len, d->nstripes, static_cast<const uint8_t*>(d->base),
+        d->strip_stride, d->stripe_stride, fail, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail_hip(e, "launch_reconstruct_strided");
+}
+
 // ---------------------------------------------------------------- runtime
 
 int draid_ec_abi_version(void) { return DRAID_EC_ABI_VERSION; }

@@ -9,6 +9,14 @@
 // concurrently (separate SDMA engines for H2D and D2H).  Stream order alone
 // protects each staging area: its next chunk's copy-in is queued behind its
 // previous chunk's copy-out.  The calls are synchronous.
+//
+// When the stripes are pinned or registered host memory (what SPDK's hugepage
+// buffers become after draid_ec_host_register) the staging is skipped: one
+// launch over the strided layout reads the strips it needs in place over PCIe
+// and writes the results straight back.  Measured on MI355X (8+2 x 64 KiB x
+// 4096, profiles/r01/host_path.json): encode 52 GiB/s and reconstruct 52 GiB/s
+// of user data -- PCIe-read bound (55.8 GB/s) -- against 50 and 35 GiB/s
+// staged, because a reconstruct reads only the k surviving strips.
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <string.h>
@@ -37,9 +45,15 @@ struct Stage {
 struct HostEngine {
     int device = -1;
     Stage st[kStreams];
+    uint8_t* zfail = nullptr;  // device copy of the fail table (zero-copy path)
+    size_t zfail_bytes = 0;
     ~HostEngine() { reset(); }
     void reset()
     {
+        if (zfail)
+            (void)hipFree(zfail);
+        zfail = nullptr;
+        zfail_bytes = 0;
         for (Stage& s : st) {
             if (s.stream)
                 (void)hipStreamSynchronize(s.stream);
@@ -108,10 +122,68 @@ int check_host(const draid_ec_host_stripes* h)
 {
     if (!h || !h->base)
         return draid::fail_arg("host stripes descriptor / base is NULL");
-    if (h->k < 1 || h->k > 255 || h->m < 1 || h->m > 2 || h->flags != 0)
-        return draid::fail_arg("host stripes need 1 <= k <= 255, m in {1,2}, flags == 0");
+    if (h->k < 1 || h->k > 255 || h->m < 1 || h->m > 2 || (h->flags & ~DRAID_EC_HOST_STAGED))
+        return draid::fail_arg("host stripes need 1 <= k <= 255, m in {1,2}, flags in {0, "
+                               "DRAID_EC_HOST_STAGED}");
     if (h->strip_stride < h->strip_len)
         return draid::fail_arg("strip_stride < strip_len");
+    return 0;
+}
+
+HostEngine& engine()
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (t_eng.device != dev) {
+        t_eng.reset();
+        t_eng.device = dev;
+    }
+    return t_eng;
+}
+
+// Device address of a host range mapped into the GPU as one piece (hipHostMalloc
+// or hipHostRegister), or nullptr for pageable memory.
+uint8_t* mapped_range(const void* p, uint64_t span)
+{
+    auto dev_addr = [](const void* q) -> uint8_t* {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        if (a.type != hipMemoryTypeHost || !a.devicePointer)
+            return nullptr;
+        // devicePointer pairs with hostPointer (which may be the allocation base)
+        const uint8_t* hp = a.hostPointer ? static_cast<const uint8_t*>(a.hostPointer)
+                                          : static_cast<const uint8_t*>(q);
+        return static_cast<uint8_t*>(a.devicePointer) + (static_cast<const uint8_t*>(q) - hp);
+    };
+    uint8_t* d0 = dev_addr(p);
+    if (!d0)
+        return nullptr;
+    uint8_t* d1 = dev_addr(static_cast<const uint8_t*>(p) + (span - 1));
+    return d1 == d0 + (span - 1) ? d0 : nullptr;
+}
+
+uint64_t host_span(const draid_ec_host_stripes* h)
+{
+    return static_cast<uint64_t>(h->nstripes - 1) * h->stripe_stride +
+           static_cast<uint64_t>(h->k + h->m - 1) * h->strip_stride + h->strip_len;
+}
+
+// In-place path over mapped host stripes: one launch, then wait.
+template <class Launch>
+int run_mapped(Launch&& launch)
+{
+    HostEngine& eng = engine();
+    Stage& s = eng.st[0];
+    hipError_t e;
+    if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
+        return draid::fail_hip(e, "hipStreamCreate(host engine)");
+    if ((e = launch(eng, s.stream)) != hipSuccess)
+        return draid::fail_hip(e, "launch (mapped host stripes)");
+    if ((e = hipStreamSynchronize(s.stream)) != hipSuccess)
+        return draid::fail_hip(e, "hipStreamSynchronize(mapped host stripes)");
     return 0;
 }
 
@@ -126,12 +198,7 @@ int run_chunks(const draid_ec_host_stripes* h, uint32_t chunk, uint32_t in_lo, u
     if (chunk == 0)
         chunk = 64;
     chunk = std::min(chunk, std::max<uint32_t>(1, h->nstripes));
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (t_eng.device != dev) {
-        t_eng.reset();
-        t_eng.device = dev;
-    }
+    (void)engine();
     for (Stage& s : t_eng.st) {
         int rc = prepare(s, k, m, S, chunk);
         if (rc)
@@ -171,6 +238,12 @@ int draid_ec_host_encode(const draid_ec_host_stripes* h, uint32_t chunk_stripes)
         return rc;
     const uint32_t k = h->k, m = h->m, n = k + m;
     const uint64_t S = h->strip_len;
+    if (!(h->flags & DRAID_EC_HOST_STAGED))
+        if (uint8_t* d = mapped_range(h->base, host_span(h)))
+            return run_mapped([&](HostEngine&, hipStream_t st) {
+                return draid::launch_encode_strided(k, m, S, h->nstripes, d, h->strip_stride,
+                                                    h->stripe_stride, st);
+            });
     return run_chunks(
         h, chunk_stripes, 0, k,
         [&](Stage& s, uint32_t, uint32_t rows) {
@@ -200,6 +273,27 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
         return draid::fail_arg("host reconstruct: fail table is NULL");
     const uint32_t k = h->k, m = h->m, n = k + m;
     const uint64_t S = h->strip_len;
+    if (!(h->flags & DRAID_EC_HOST_STAGED))
+        if (uint8_t* d = mapped_range(h->base, host_span(h)))
+            return run_mapped([&](HostEngine& eng, hipStream_t st) {
+                const size_t fb = 2 * static_cast<size_t>(h->nstripes);
+                hipError_t e;
+                if (eng.zfail_bytes < fb) {
+                    if (eng.zfail)
+                        (void)hipFree(eng.zfail);
+                    eng.zfail = nullptr;
+                    eng.zfail_bytes = 0;
+                    if ((e = hipMalloc(&eng.zfail, fb)) != hipSuccess)
+                        return e;
+                    eng.zfail_bytes = fb;
+                }
+                if ((e = hipMemcpyAsync(eng.zfail, fail, fb, hipMemcpyHostToDevice, st)) !=
+                    hipSuccess)
+                    return e;
+                return draid::launch_reconstruct_strided(k, m, S, h->nstripes, d,
+                                                         h->strip_stride, h->stripe_stride,
+                                                         eng.zfail, st);
+            });
     return run_chunks(
         h, chunk_stripes, 0, n,
         [&](Stage& s, uint32_t c0, uint32_t rows) {

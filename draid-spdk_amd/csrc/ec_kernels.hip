@@ -45,6 +45,17 @@ struct TablePtrs {
     }
 };
 
+// Regular layout: strip j of stripe s at base + s*stripe_stride + j*strip_stride
+// (a stripe cache laid out as one array, or pinned host stripes read in place).
+struct StridedPtrs {
+    const uint8_t* base;
+    uint64_t strip_stride, stripe_stride;
+    __device__ __forceinline__ const uint8_t* get(uint32_t s, int j) const
+    {
+        return base + s * stripe_stride + static_cast<uint64_t>(j) * strip_stride;
+    }
+};
+
 struct ArgPtrs {
     ArgPtrTable t;
     __device__ __forceinline__ const uint8_t* get(uint32_t, int j) const { return t.p[j]; }
@@ -879,6 +890,27 @@ hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nst
     if (m == 1)
         return dispatch_reconstruct<1>(pp, k, len, 1, fail_dev, f01, st);
     return dispatch_reconstruct<2>(pp, k, len, 1, fail_dev, f01, st);
+}
+
+hipError_t launch_encode_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                                 const uint8_t* base, uint64_t strip_stride,
+                                 uint64_t stripe_stride, hipStream_t st)
+{
+    const StridedPtrs pp{base, strip_stride, stripe_stride};
+    if (m == 1)
+        return dispatch_encode<1>(pp, k, len, nstripes, st);
+    return dispatch_encode<2>(pp, k, len, nstripes, st);
+}
+
+hipError_t launch_reconstruct_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                                      const uint8_t* base, uint64_t strip_stride,
+                                      uint64_t stripe_stride, const uint8_t* fail_dev,
+                                      hipStream_t st)
+{
+    const StridedPtrs pp{base, strip_stride, stripe_stride};
+    if (m == 1)
+        return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, 0xffff, st);
+    return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, 0xffff, st);
 }
 
 hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* const* table,

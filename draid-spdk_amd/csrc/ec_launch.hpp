@@ -22,6 +22,15 @@ hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes
                          const uint8_t* const* table, const ArgPtrTable* args,
                          hipStream_t stream);
 
+// Strided layout: strip j of stripe s at base + s*stripe_stride + j*strip_stride.
+hipError_t launch_encode_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                                 const uint8_t* base, uint64_t strip_stride,
+                                 uint64_t stripe_stride, hipStream_t stream);
+hipError_t launch_reconstruct_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
+                                      const uint8_t* base, uint64_t strip_stride,
+                                      uint64_t stripe_stride, const uint8_t* fail_dev,
+                                      hipStream_t stream);
+
 // Reconstruct.  fail_dev: device [nstripes][2] (0xFF = none); when null,
 // (f0, f1) apply to every stripe.
 hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,

@@ -30,6 +30,7 @@ EXPORTS = (
     "draid_ec_ctx_stream", "draid_ec_ctx_encode_sg", "draid_ec_ctx_reconstruct_sg",
     "draid_ec_ctx_flush", "draid_ec_ctx_query", "draid_ec_ctx_synchronize",
     "draid_ec_ctx_queued", "draid_ec_host_encode", "draid_ec_host_reconstruct",
+    "draid_ec_encode_strided", "draid_ec_reconstruct_strided",
     "draid_ec_ctx_update_sg",
 )
 
@@ -113,6 +114,8 @@ def lib() -> C.CDLL:
                                                   C.c_size_t, i32, vp]
         L.draid_ec_ctx_update_sg.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp,
                                              vp, vp, vp, vp, C.c_size_t]
+        L.draid_ec_encode_strided.argtypes = [C.POINTER(HostStripes), vp]
+        L.draid_ec_reconstruct_strided.argtypes = [C.POINTER(HostStripes), vp, vp]
         L.draid_ec_host_encode.argtypes = [C.POINTER(HostStripes), C.c_uint32]
         L.draid_ec_host_reconstruct.argtypes = [C.POINTER(HostStripes), vp, C.c_uint32]
         _lib = L
@@ -214,14 +217,31 @@ def stream_synchronize(stream: int) -> None:
 
 # ---- host-resident stripes ----
 
-def host_encode(base, k, m, strip_len, nstripes, strip_stride, stripe_stride, chunk=0) -> int:
-    h = HostStripes(k, m, strip_len, nstripes, 0, _ptr(base), strip_stride, stripe_stride)
+def encode_strided(base, k, m, strip_len, nstripes, strip_stride, stripe_stride,
+                   stream: int) -> int:
+    d = HostStripes(k, m, strip_len, nstripes, 0, _ptr(base), strip_stride, stripe_stride)
+    return _check(lib().draid_ec_encode_strided(C.byref(d), stream), "encode_strided")
+
+
+def reconstruct_strided(base, k, m, strip_len, nstripes, strip_stride, stripe_stride, fail,
+                        stream: int) -> int:
+    d = HostStripes(k, m, strip_len, nstripes, 0, _ptr(base), strip_stride, stripe_stride)
+    return _check(lib().draid_ec_reconstruct_strided(C.byref(d), _ptr(fail), stream),
+                  "reconstruct_strided")
+
+
+HOST_STAGED = 1
+
+
+def host_encode(base, k, m, strip_len, nstripes, strip_stride, stripe_stride, chunk=0,
+                flags=0) -> int:
+    h = HostStripes(k, m, strip_len, nstripes, flags, _ptr(base), strip_stride, stripe_stride)
     return _check(lib().draid_ec_host_encode(C.byref(h), chunk), "host_encode")
 
 
 def host_reconstruct(base, k, m, strip_len, nstripes, strip_stride, stripe_stride, fail,
-                     chunk=0) -> int:
-    h = HostStripes(k, m, strip_len, nstripes, 0, _ptr(base), strip_stride, stripe_stride)
+                     chunk=0, flags=0) -> int:
+    h = HostStripes(k, m, strip_len, nstripes, flags, _ptr(base), strip_stride, stripe_stride)
     return _check(lib().draid_ec_host_reconstruct(C.byref(h), _ptr(fail), chunk),
                   "host_reconstruct")
 

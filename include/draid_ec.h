@@ -112,6 +112,26 @@ int draid_ec_encode(const draid_ec_stripe_batch *batch, void *stream);
 int draid_ec_reconstruct(const draid_ec_stripe_batch *batch, const uint8_t *fail,
                          void *stream);
 
+/* Regular layout, no pointer table: strip j of stripe s at
+ * base + s*stripe_stride + j*strip_stride (a stripe cache allocated as one
+ * array, raid5.c:1331-1353 with the n chunk buffers of a stripe adjacent). */
+typedef struct draid_ec_strided_stripes {
+    uint32_t k, m;           /* as draid_ec_stripe_batch                          */
+    uint64_t strip_len;      /* bytes per strip                                   */
+    uint32_t nstripes;
+    uint32_t flags;          /* 0, or DRAID_EC_HOST_STAGED for the 2c host calls  */
+    void *base;
+    uint64_t strip_stride;   /* >= strip_len                                      */
+    uint64_t stripe_stride;
+} draid_ec_strided_stripes;
+
+/* As draid_ec_encode / draid_ec_reconstruct over a strided layout.  `base` is
+ * device memory, or pinned / registered host memory (read in place over PCIe).
+ * `fail` is a DEVICE array as above. */
+int draid_ec_encode_strided(const draid_ec_strided_stripes *s, void *stream);
+int draid_ec_reconstruct_strided(const draid_ec_strided_stripes *s, const uint8_t *fail,
+                                 void *stream);
+
 /* ------------------------------------------------------------------------
  * 2b. Scatter-gather stripes through a per-channel context
  *
@@ -163,22 +183,19 @@ uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last
 /* ------------------------------------------------------------------------
  * 2c. Host-resident stripes (PCIe-inclusive path)
  *
- * SPDK's stripe buffers are host hugepages.  These calls copy the input strips
- * in (hipMemcpy2DAsync per strip index over a chunk of stripes), run the kernel
- * in HBM and copy the results back, pipelined over three streams.  Register or
- * pin the host range first (draid_ec_host_register) for full PCIe speed.
- * Synchronous.  chunk_stripes = stripes per pipeline stage (0 = 64).
+ * SPDK's stripe buffers are host hugepages.  When the whole range is pinned or
+ * registered (draid_ec_host_register) the kernel reads the strips it needs in
+ * place over PCIe and writes P/Q (or the rebuilt strips) straight back: one
+ * launch, no staging -- a reconstruct moves only the surviving strips.  For
+ * pageable memory, or with flags = DRAID_EC_HOST_STAGED, the calls copy the
+ * input strips in (hipMemcpy2DAsync per strip index over a chunk of stripes),
+ * run the kernel in HBM and copy the results back, pipelined over three
+ * streams; chunk_stripes = stripes per pipeline stage (0 = 64).  Synchronous.
  * ---------------------------------------------------------------------- */
 
-typedef struct draid_ec_host_stripes {
-    uint32_t k, m;           /* as draid_ec_stripe_batch                          */
-    uint64_t strip_len;      /* bytes per strip                                   */
-    uint32_t nstripes;
-    uint32_t flags;          /* reserved, must be 0                               */
-    void *base;              /* HOST: strip j of stripe s at                      */
-    uint64_t strip_stride;   /*   base + s*stripe_stride + j*strip_stride         */
-    uint64_t stripe_stride;
-} draid_ec_host_stripes;
+#define DRAID_EC_HOST_STAGED 1u
+
+typedef draid_ec_strided_stripes draid_ec_host_stripes;   /* base is HOST memory */
 
 /* Data strips in, P (and Q) out. */
 int draid_ec_host_encode(const draid_ec_host_stripes *h, uint32_t chunk_stripes);

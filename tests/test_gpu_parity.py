@@ -335,3 +335,70 @@ def test_full_size_roundtrip(ec, k, m, L, B):
     assert ec.reconstruct(b.batch(ec), fd, stream) == 0
     sync()
     assert torch.equal(b.strips(), good)
+
+
+# ------------------------------------------------------------ edge buffers
+
+def _edge_stripes(k, m, L):
+    """SURVEY.md §8(d) edge buffers: all-0x00, all-0xFF, one set bit per stripe
+    (every bit position and every data strip), and the raid5_ut_ref pattern
+    (0xFF fill + 8-byte LE block index, raid5_ut_ref.c:324-330)."""
+    n = k + m
+    rows = [np.zeros((n, L), np.uint8)]
+    full = np.zeros((n, L), np.uint8)
+    full[:k] = 0xFF
+    rows.append(full)
+    for j in range(k):
+        for bit in range(8):
+            r = np.zeros((n, L), np.uint8)
+            r[j, (j * 131 + bit * 17) % L] = 1 << bit
+            rows.append(r)
+    ut = np.zeros((n, L), np.uint8)
+    ut[:k] = oracle.ut_ref_pattern(k * L // 512, 512).reshape(k, L)
+    rows.append(ut)
+    return np.stack(rows)
+
+
+@pytest.mark.parametrize("k,m", [(4, 1), (8, 2), (16, 2)])
+def test_edge_buffers(ec, k, m):
+    L = 4096
+    data = _edge_stripes(k, m, L)
+    B = data.shape[0]
+    ref = oracle_encode(data, k, m)
+    if m == 2:  # all-0xFF: P = 0xFF iff k odd; Q = xor of 2^j * 0xFF
+        assert (ref[1, k] == (0xFF if k % 2 else 0)).all()
+    b = Batch(k, m, L, B, data=data)
+    stream = torch.cuda.current_stream().cuda_stream
+    assert ec.encode(b.batch(ec), stream) == 0
+    sync()
+    assert (host(b.strips()) == ref).all()
+    # every failure pair, cycled over the edge stripes
+    n = k + m
+    pairs = [(x, 0xFF) for x in range(n)]
+    if m == 2:
+        pairs += [(x, y) for x in range(n) for y in range(x + 1, n)]
+    for p0 in range(0, len(pairs), B):
+        fail = np.array([pairs[(p0 + s) % len(pairs)] for s in range(B)], np.uint8)
+        v = b.strips()
+        for s in range(B):
+            for f in fail[s]:
+                if f != 0xFF:
+                    v[s, int(f)].fill_(0xA5)
+        assert ec.reconstruct(b.batch(ec), dev(fail.reshape(-1)), stream) == 0
+        sync()
+        assert (host(b.strips()) == ref).all()
+
+
+@pytest.mark.parametrize("k,m,L,B", [(8, 2, 65536, 4096), (16, 2, 262144, 512)])
+def test_full_size_linearity(ec, k, m, L, B):
+    """Parity is GF(2)-linear: encode(A ^ C) == encode(A) ^ encode(C) over the whole
+    BASELINE-sized batch (a size-independent check of every stripe's P and Q)."""
+    a = Batch(k, m, L, B, seed=5)
+    c = Batch(k, m, L, B, seed=6)
+    stream = torch.cuda.current_stream().cuda_stream
+    x = Batch(k, m, L, B, data=None, seed=7)
+    x.strips()[:, :k] = a.strips()[:, :k] ^ c.strips()[:, :k]
+    for t in (a, c, x):
+        assert ec.encode(t.batch(ec), stream) == 0
+    sync()
+    assert torch.equal(x.strips()[:, k:], a.strips()[:, k:] ^ c.strips()[:, k:])

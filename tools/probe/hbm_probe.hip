@@ -57,3 +57,48 @@ int probe_copy(const void* src, void* dst, uint64_t bytes, int grid, void* strea
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }
+
+// Stripe-pattern probe: the encode kernel's memory pattern without its math.
+// Block b -> stripe s = b / cps, chunk c = b % cps (4 KiB of every strip); each
+// lane loads K 16-B vectors at stride S, XORs them, and stores the result to
+// the M strips after the data (M = 0: pure read, result stored only if it is an
+// impossible value).
+template <int KT>
+__global__ __launch_bounds__(256) void k_stripe_pattern(uint8_t* base, uint64_t S,
+                                                        uint64_t stripe_stride, int K, int M,
+                                                        uint32_t cps, u32x4* sink)
+{
+    const uint32_t s = blockIdx.x / cps, c = blockIdx.x % cps;
+    uint8_t* st = base + s * stripe_stride + (uint64_t)c * 4096 + threadIdx.x * 16;
+    u32x4 acc = 0;
+    if constexpr (KT > 0) {
+        u32x4 v[KT];
+#pragma unroll
+        for (int j = 0; j < KT; ++j)
+            v[j] = __builtin_nontemporal_load((const u32x4*)(st + j * S));
+#pragma unroll
+        for (int j = 0; j < KT; ++j)
+            acc ^= v[j];
+        K = KT;
+    } else {
+        for (int j = 0; j < K; ++j)
+            acc ^= __builtin_nontemporal_load((const u32x4*)(st + j * S));
+    }
+    if (M == 0) {
+        if ((acc.x & acc.y & acc.z & acc.w) == 0xfffffffeu)
+            sink[blockIdx.x & 1023] = acc;
+        return;
+    }
+    for (int j = 0; j < M; ++j)
+        __builtin_nontemporal_store(acc, (u32x4*)(st + (K + j) * S));
+}
+
+extern "C" int probe_stripe_pattern(void* base, uint64_t S, uint64_t stripe_stride, int K, int M,
+                                    uint32_t nstripes, void* sink, void* stream)
+{
+    const uint32_t cps = (uint32_t)(S / 4096);
+    auto kern = K == 8 ? k_stripe_pattern<8> : K == 16 ? k_stripe_pattern<16> : k_stripe_pattern<0>;
+    hipLaunchKernelGGL(kern, dim3(cps * nstripes), dim3(256), 0, (hipStream_t)stream,
+                       (uint8_t*)base, S, stripe_stride, K, M, cps, (u32x4*)sink);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
