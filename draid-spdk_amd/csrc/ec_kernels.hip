@@ -215,6 +215,14 @@ __device__ __forceinline__ void item_coords(uint32_t b, uint32_t cps, uint32_t n
     if constexpr (C::MAP == 1) {
         c = b / nstripes;
         s = b - c * nstripes;
+    } else if constexpr (C::MAP == 3) {
+        // XCD-aware: the dispatcher deals workgroup b to XCD b % 8; give each XCD a
+        // contiguous run of items (whole stripes) instead of every 8th chunk.
+        const uint32_t total = cps * nstripes, q = total >> 3, r = total & 7u;
+        const uint32_t x = b & 7u, i = b >> 3;
+        const uint32_t bb = x * q + min(x, r) + i;
+        s = bb / cps;
+        c = bb - s * cps;
     } else {
         s = b / cps;
         c = b - s * cps;
@@ -813,8 +821,11 @@ using V12 = Cfg<256, 4, 3, 0, 0>;  // U=4
 using V13 = Cfg<256, 2, 3, 0, 2>;  // DIAGNOSTIC: reconstruct without the plan step, U=2
 using V14 = Cfg<256, 1, 3, 0, 2>;  // DIAGNOSTIC: reconstruct without the plan step, U=1
 using V15 = Cfg<256, 1, 3, 0, 3>;  // DIAGNOSTIC: no plan step and no GF multiplies, U=1
+using V16 = Cfg<256, 1, 3, 3, 0>;  // XCD-aware item order
+using V17 = Cfg<512, 1, 3, 3, 0>;  // XCD-aware, 512 lanes
 #define DRAID_VARIANTS(X) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5) X(6, V6) X(7, V7) X(8, V8) \
-    X(9, V9) X(10, V10) X(11, V11) X(12, V12) X(13, V13) X(14, V14) X(15, V15)
+    X(9, V9) X(10, V10) X(11, V11) X(12, V12) X(13, V13) X(14, V14) X(15, V15) X(16, V16)     \
+    X(17, V17)
 
 template <int K, int M>
 static hipError_t variant_encode(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
