@@ -765,10 +765,19 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
     return hipGetLastError();
 }
 
-// Production configuration: 256 lanes, non-temporal loads and stores,
-// one item per workgroup, LDS-staged GF tables.
+// Production configuration: one wave (64 lanes) per workgroup, non-temporal
+// loads and stores, one item per workgroup, LDS-staged GF tables.  A one-wave
+// item is 1 KiB of every strip of a stripe.  Measured against 256 lanes
+// (tools/sweep.py, profiles/r01/sweepx_*.json, stripe-major, median of 5 rounds):
+// reconstruct +2..5% at every BASELINE shape (8+2 x 64 KiB dual 6580 vs 6295
+// GB/s), encode +5% for 4+1 x 64 KiB and 8+2 x 128 KiB and within 0.5% for
+// 8+2 x 64 KiB and 16+2 x 256 KiB.  Small workgroups retire independently, so a
+// CU refills a finished wave's slot immediately instead of waiting for the
+// slowest wave of a 4-wave group, and the table-staging barrier is a single
+// wave's.
+constexpr int kLanes = 64;
 template <int U>
-using CfgDefault = Cfg<256, U, 3, 0, 0>;
+using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;
 
 // k values with a fully unrolled instantiation; others use the runtime-k loop.
 #define DRAID_FOR_EACH_K(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(12) X(14) X(16)
@@ -823,9 +832,12 @@ using V14 = Cfg<256, 1, 3, 0, 2>;  // DIAGNOSTIC: reconstruct without the plan s
 using V15 = Cfg<256, 1, 3, 0, 3>;  // DIAGNOSTIC: no plan step and no GF multiplies, U=1
 using V16 = Cfg<256, 1, 3, 3, 0>;  // XCD-aware item order
 using V17 = Cfg<512, 1, 3, 3, 0>;  // XCD-aware, 512 lanes
+using V18 = Cfg<64, 2, 3, 0, 0>;   // one wave, U=2
+using V19 = Cfg<64, 4, 3, 0, 0>;   // one wave, U=4
+using V20 = Cfg<64, 1, 3, 3, 0>;   // one wave, XCD-aware
 #define DRAID_VARIANTS(X) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5) X(6, V6) X(7, V7) X(8, V8) \
     X(9, V9) X(10, V10) X(11, V11) X(12, V12) X(13, V13) X(14, V14) X(15, V15) X(16, V16)     \
-    X(17, V17)
+    X(17, V17) X(18, V18) X(19, V19) X(20, V20)
 
 template <int K, int M>
 static hipError_t variant_encode(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,
@@ -967,7 +979,7 @@ static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t k,
 uint32_t work_chunk_bytes(int op, uint32_t k)
 {
     if (op == 2)
-        return 256u * 1u * 16u;  // update: CfgDefault<1>
+        return kLanes * 1u * 16u;  // update: CfgDefault<1>
     int u = 2;
     switch (k) {
 #define DRAID_CASE(K)                                       \
@@ -979,7 +991,7 @@ uint32_t work_chunk_bytes(int op, uint32_t k)
     default:
         break;
     }
-    return 256u * static_cast<uint32_t>(u) * 16u;
+    return kLanes * static_cast<uint32_t>(u) * 16u;
 }
 
 hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,

@@ -9,7 +9,7 @@ CFGS=${@:-raid6_8p2_64k raid5_4p1_64k raid6_8p2_128k_single raid6_16p2_256k_dual
 for c in $CFGS; do
   O=gpurun_out/cfg_$c
   rm -rf $O; mkdir -p $O
-  B="python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-verify"
+  B="python3 bench.py --config $c --steps 50 --warmup 10 --no-cpu-baseline --no-verify"
   echo "== $c bench $(date +%T)"
   timeout -k 10 300 python3 bench.py --config $c --cpu-seconds 5 > $O/bench.log 2>&1 || { tail $O/bench.log; exit 1; }
   tail -1 $O/bench.log

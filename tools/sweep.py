@@ -20,11 +20,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "draid-spdk_amd"))
 sys.path.insert(0, ROOT)
 
-VARIANTS = {0: "default (enc U1, rec U2)", 1: "U2", 2: "512 lanes U1", 3: "128 lanes",
+VARIANTS = {0: "default (64 lanes U1)", 1: "U2", 2: "512 lanes U1", 3: "128 lanes",
             4: "chunk-major map", 5: "persistent", 6: "scalar plan", 7: "persist 512 scalar",
-            8: "1024 lanes", 9: "64 lanes", 10: "U1", 11: "512 lanes U2", 12: "U4",
+            8: "1024 lanes", 9: "64 lanes", 10: "256 lanes U1", 11: "512 lanes U2", 12: "U4",
             13: "DIAG no-plan U2", 14: "DIAG no-plan U1", 15: "DIAG no-plan no-mul U1",
-            16: "XCD-aware map", 17: "XCD-aware 512 lanes"}
+            16: "XCD-aware map", 17: "XCD-aware 512 lanes",
+            18: "64 lanes U2", 19: "64 lanes U4", 20: "64 lanes XCD-aware"}
 
 
 def probe(torch, dev, nbytes, rounds, iters):
