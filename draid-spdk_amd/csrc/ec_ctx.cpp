@@ -151,18 +151,30 @@ int flush_group(draid_ec_ctx* c, Group& g)
     if (nseg == 0)
         return 0;
     const uint32_t cb = draid::work_chunk_bytes(g.op, g.k);
+    // Uniform segments (every run the same length: whole strips, fixed-size
+    // iovecs) need no work list -- the kernel derives (segment, chunk) itself.
+    const bool uniform = std::all_of(g.len.begin(), g.len.end(),
+                                     [&](uint32_t l) { return l == g.len[0]; });
     std::vector<uint32_t> work;  // pairs {seg, chunk}
-    for (size_t s = 0; s < nseg; ++s) {
-        const uint32_t cps = std::max<uint32_t>(1, (g.len[s] + cb - 1) / cb);
-        for (uint32_t ch = 0; ch < cps; ++ch) {
-            work.push_back(static_cast<uint32_t>(s));
-            work.push_back(ch);
+    uint64_t nwork64;
+    if (uniform) {
+        nwork64 = static_cast<uint64_t>(nseg) * std::max<uint32_t>(1, (g.len[0] + cb - 1) / cb);
+    } else {
+        for (size_t s = 0; s < nseg; ++s) {
+            const uint32_t cps = std::max<uint32_t>(1, (g.len[s] + cb - 1) / cb);
+            for (uint32_t ch = 0; ch < cps; ++ch) {
+                work.push_back(static_cast<uint32_t>(s));
+                work.push_back(ch);
+            }
         }
+        nwork64 = work.size() / 2;
     }
-    const uint32_t nwork = static_cast<uint32_t>(work.size() / 2);
+    if (nwork64 > 0x7fffffffull)
+        return ctx_arg("flush: too many work items queued (flush more often)");
+    const uint32_t nwork = static_cast<uint32_t>(nwork64);
     const size_t o_ptr = 0;
     const size_t o_len = align8(o_ptr + g.ptrs.size() * sizeof(void*));
-    const size_t o_fail = align8(o_len + nseg * sizeof(uint32_t));
+    const size_t o_fail = align8(o_len + (uniform ? 0 : nseg * sizeof(uint32_t)));
     const size_t o_work = align8(o_fail + g.fail.size());
     const size_t bytes = o_work + work.size() * sizeof(uint32_t);
 
@@ -190,23 +202,27 @@ int flush_group(draid_ec_ctx* c, Group& g)
     }
     uint8_t* h = static_cast<uint8_t*>(sl.host);
     memcpy(h + o_ptr, g.ptrs.data(), g.ptrs.size() * sizeof(void*));
-    memcpy(h + o_len, g.len.data(), nseg * sizeof(uint32_t));
+    if (!uniform)
+        memcpy(h + o_len, g.len.data(), nseg * sizeof(uint32_t));
     if (!g.fail.empty())
         memcpy(h + o_fail, g.fail.data(), g.fail.size());
-    memcpy(h + o_work, work.data(), work.size() * sizeof(uint32_t));
+    if (!work.empty())
+        memcpy(h + o_work, work.data(), work.size() * sizeof(uint32_t));
     if ((e = hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, c->stream)) !=
         hipSuccess)
         return ctx_fail(e, "hipMemcpyAsync(descriptors)");
     const uint8_t* d = static_cast<const uint8_t*>(sl.dev);
     const auto* tab = reinterpret_cast<const uint8_t* const*>(d + o_ptr);
     const auto* lens = reinterpret_cast<const uint32_t*>(d + o_len);
+    const void* wl = uniform ? nullptr : d + o_work;
+    const uint32_t ulen = g.len[0];
     if (g.op == 0)
-        e = draid::launch_encode_work(g.k, g.m, tab, lens, d + o_work, nwork, c->stream);
+        e = draid::launch_encode_work(g.k, g.m, tab, lens, wl, ulen, nwork, c->stream);
     else if (g.op == 1)
-        e = draid::launch_reconstruct_work(g.k, g.m, tab, lens, d + o_fail, d + o_work, nwork,
+        e = draid::launch_reconstruct_work(g.k, g.m, tab, lens, d + o_fail, wl, ulen, nwork,
                                            c->stream);
     else
-        e = draid::launch_update_work(g.m, g.k / 2, tab, d + o_fail, lens, d + o_work, nwork,
+        e = draid::launch_update_work(g.m, g.k / 2, tab, d + o_fail, lens, wl, ulen, nwork,
                                       c->stream);
     if (e != hipSuccess)
         return ctx_fail(e, "launch (segment work list)");

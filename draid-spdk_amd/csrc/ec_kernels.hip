@@ -444,6 +444,35 @@ __device__ __forceinline__ void stage_gf_tables(LdsGf& lds)
     __syncthreads();
 }
 
+// The GF tables staged through registers: each lane loads its words FIRST, before
+// any strip load (vmcnt retires in issue order, so the LDS write then waits only
+// for them, not for the strip loads issued after), and writes them to LDS once
+// its strip loads are in flight -- staging and barrier overlap the loads.
+template <int NTHR>
+struct TabStage {
+    static constexpr int kWords = (512 + 256) / 4;
+    static constexpr int kPerLane = (kWords + NTHR - 1) / NTHR;
+    uint32_t w[kPerLane];
+    __device__ __forceinline__ void load()
+    {
+#pragma unroll
+        for (int i = 0; i < kPerLane; ++i) {
+            const int t = threadIdx.x + i * NTHR;
+            w[i] = t < kWords ? reinterpret_cast<const uint32_t*>(&c_gf)[t] : 0u;
+        }
+    }
+    __device__ __forceinline__ void store(LdsGf& lds) const
+    {
+#pragma unroll
+        for (int i = 0; i < kPerLane; ++i) {
+            const int t = threadIdx.x + i * NTHR;
+            if (t < kWords)
+                lds.w[t] = w[i];
+        }
+        __syncthreads();
+    }
+};
+
 template <int KT, int M, class C, class Ptrs, class F>
 __device__ __forceinline__ void reconstruct_item(const Ptrs& pp, uint32_t s, uint32_t c, int k,
                                                  uint32_t len, uint32_t cps, RecPlan& pl,
@@ -491,21 +520,9 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
     const uint32_t total = cps * nstripes;
     if constexpr (C::MAP == 2)
         stage_gf_tables<C::NTHR>(lds);  // once per persistent workgroup
-    // The table word this lane stages is loaded FIRST: vmcnt retires in issue
-    // order, so the LDS write below then waits only for it, not for the strip
-    // loads issued after it -- staging and barrier overlap the strip loads.
-    constexpr int kTabWords = (512 + 256) / 4;
-    constexpr int kPerLane = (kTabWords + C::NTHR - 1) / C::NTHR;
-    uint32_t tab_word[kPerLane];
-#pragma unroll
-    for (int w = 0; w < kPerLane; ++w) {
-        const int t = threadIdx.x + w * C::NTHR;
-        tab_word[w] = 0;
-        if constexpr (C::MAP != 2 && C::PLAN == 0) {
-            if (t < kTabWords)
-                tab_word[w] = reinterpret_cast<const uint32_t*>(&c_gf)[t];
-        }
-    }
+    TabStage<C::NTHR> tabs;
+    if constexpr (C::MAP != 2 && C::PLAN == 0)
+        tabs.load();
     for (uint32_t b = blockIdx.x; b < total; b += (C::MAP == 2 ? gridDim.x : total)) {
         uint32_t s, c;
         item_coords<C>(b, cps, nstripes, s, c);
@@ -535,13 +552,7 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
         } else {
             // Stage the tables while this lane's strip loads are in flight.
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-#pragma unroll
-                for (int w = 0; w < kPerLane; ++w) {
-                    const int t = threadIdx.x + w * C::NTHR;
-                    if (t < kTabWords)
-                        lds.w[t] = tab_word[w];
-                }
-                __syncthreads();
+                tabs.store(lds);
                 plan_constants(p, l_exp, l_log);
             });
         }
@@ -559,43 +570,66 @@ struct WorkItem {
     uint32_t chunk;
 };
 
+// Where work item b comes from: an explicit (segment, chunk) list, or -- when
+// every queued segment has the same length (full-strip runs, fixed-size iovecs)
+// -- arithmetic, so the item costs no descriptor load at all.
+struct WorkSrc {
+    const WorkItem* list;      // nullptr: uniform segments
+    const uint32_t* seg_len;   // list mode
+    uint32_t ulen, ucps;       // uniform mode: segment length, items per segment
+    __device__ __forceinline__ void get(uint32_t b, uint32_t cb, uint32_t& seg, uint32_t& chunk,
+                                        uint32_t& len, uint32_t& cps) const
+    {
+        if (list) {
+            const WorkItem w = list[b];
+            seg = w.seg;
+            chunk = w.chunk;
+            len = seg_len[seg];
+            cps = (len + cb - 1) / cb;
+        } else {
+            seg = b / ucps;
+            chunk = b - seg * ucps;
+            len = ulen;
+            cps = ucps;
+        }
+    }
+};
+
 template <int KT, int M, bool CHECK, class C>
-__global__ __launch_bounds__(C::NTHR) void k_encode_work(TablePtrs pp, uint32_t k_rt,
-                                                         const uint32_t* seg_len,
-                                                         const WorkItem* work, uint32_t nwork)
+__global__ __launch_bounds__(C::NTHR) void k_encode_work(TablePtrs pp, uint32_t k_rt, WorkSrc ws,
+                                                         uint32_t nwork)
 {
-    constexpr uint64_t CB = static_cast<uint64_t>(C::NTHR) * C::U * 16;
+    constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
     const int k = KT > 0 ? KT : static_cast<int>(k_rt);
     for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
-        const WorkItem w = work[b];
-        const uint32_t len = seg_len[w.seg];
-        const uint32_t cps = static_cast<uint32_t>((len + CB - 1) / CB);
-        encode_item<KT, M, CHECK, C>(pp, w.seg, w.chunk, k, len, cps);
+        uint32_t seg, chunk, len, cps;
+        ws.get(b, CB, seg, chunk, len, cps);
+        encode_item<KT, M, CHECK, C>(pp, seg, chunk, k, len, cps);
     }
 }
 
 template <int KT, int M, class C>
 __global__ __launch_bounds__(C::NTHR) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
-                                                              const uint32_t* seg_len,
-                                                              const uint8_t* fail,
-                                                              const WorkItem* work,
+                                                              WorkSrc ws, const uint8_t* fail,
                                                               uint32_t nwork)
 {
     __shared__ LdsGf lds;
     const uint8_t* l_exp = reinterpret_cast<const uint8_t*>(lds.w);
     const uint8_t* l_log = l_exp + 512;
-    constexpr uint64_t CB = static_cast<uint64_t>(C::NTHR) * C::U * 16;
+    constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
     const int k = KT > 0 ? KT : static_cast<int>(k_rt);
-    stage_gf_tables<C::NTHR>(lds);
+    TabStage<C::NTHR> tabs;
+    tabs.load();
     for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
-        const WorkItem w = work[b];
-        const uint32_t len = seg_len[w.seg];
-        const uint32_t cps = static_cast<uint32_t>((len + CB - 1) / CB);
-        RecPlan pl = decode_failures<M>(k, fail[2 * (size_t)w.seg], fail[2 * (size_t)w.seg + 1]);
+        uint32_t seg, chunk, len, cps;
+        ws.get(b, CB, seg, chunk, len, cps);
+        RecPlan pl = decode_failures<M>(k, fail[2 * (size_t)seg], fail[2 * (size_t)seg + 1]);
         if (pl.skip)
             continue;
-        reconstruct_item<KT, M, C>(pp, w.seg, w.chunk, k, len, cps, pl,
-                                   [&](RecPlan& p) { plan_constants(p, l_exp, l_log); });
+        reconstruct_item<KT, M, C>(pp, seg, chunk, k, len, cps, pl, [&](RecPlan& p) {
+            tabs.store(lds);
+            plan_constants(p, l_exp, l_log);
+        });
     }
 }
 
@@ -611,15 +645,15 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct_work(TablePtrs pp, uint
 // Segment table row: [O_0, N_0, O_1, N_1, ..., P, (Q)]; exps row: e_0 > e_1 > ...
 template <int M, class C>
 __global__ __launch_bounds__(C::NTHR) void k_update_work(const uint8_t* const* tab, uint32_t nd,
-                                                         const uint8_t* exps,
-                                                         const uint32_t* seg_len,
-                                                         const WorkItem* work, uint32_t nwork)
+                                                         const uint8_t* exps, WorkSrc ws,
+                                                         uint32_t nwork)
 {
     constexpr uint32_t EPB = static_cast<uint32_t>(C::NTHR) * C::U;
     const uint32_t stride = 2 * nd + M;
     for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
-        const WorkItem w = work[b];
-        const uint32_t len = seg_len[w.seg];
+        WorkItem w;
+        uint32_t len, cps_w;
+        ws.get(b, EPB * 16, w.seg, w.chunk, len, cps_w);
         const uint8_t* const* row = tab + (size_t)w.seg * stride;
         const uint8_t* ex = exps + (size_t)w.seg * nd;
         const uint8_t* pP = row[2 * nd];
@@ -659,7 +693,7 @@ __global__ __launch_bounds__(C::NTHR) void k_update_work(const uint8_t* const* t
                     body(u32x4{}, i);
             }
             const uint32_t tail = len & 15u;
-            const uint32_t cps = (len + EPB * 16 - 1) / (EPB * 16);
+            const uint32_t cps = cps_w;
             if (tail && w.chunk == cps - 1 && threadIdx.x < tail)
                 body(uint32_t{}, nvec * 16 + threadIdx.x);
         } else {
@@ -951,28 +985,39 @@ hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* con
 
 // ---- segment work lists
 
+// Work source for a launch: the explicit list, or uniform segments of `ulen`
+// bytes when `work` is null.
+template <class C>
+static WorkSrc work_src(const uint32_t* seg_len, const void* work, uint32_t ulen)
+{
+    constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
+    WorkSrc ws{static_cast<const WorkItem*>(work), seg_len, ulen, 1};
+    if (!work)
+        ws.ucps = ulen ? (ulen + CB - 1) / CB : 1;
+    return ws;
+}
+
 template <int KT, int M, class C>
 static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, const uint32_t* seg_len,
-                                 const void* work, uint32_t nwork, hipStream_t st)
+                                 const void* work, uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
     if (nwork == 0)
         return hipSuccess;
     hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                       TablePtrs{tab, k + M}, k, seg_len, static_cast<const WorkItem*>(work),
-                       nwork);
+                       TablePtrs{tab, k + M}, k, work_src<C>(seg_len, work, ulen), nwork);
     return hipGetLastError();
 }
 
 template <int KT, int M, class C>
 static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t k,
                                       const uint32_t* seg_len, const uint8_t* fail,
-                                      const void* work, uint32_t nwork, hipStream_t st)
+                                      const void* work, uint32_t ulen, uint32_t nwork,
+                                      hipStream_t st)
 {
     if (nwork == 0)
         return hipSuccess;
     hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                       TablePtrs{tab, k + M}, k, seg_len, fail,
-                       static_cast<const WorkItem*>(work), nwork);
+                       TablePtrs{tab, k + M}, k, work_src<C>(seg_len, work, ulen), fail, nwork);
     return hipGetLastError();
 }
 
@@ -995,57 +1040,60 @@ uint32_t work_chunk_bytes(int op, uint32_t k)
 }
 
 hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,
-                              const uint32_t* seg_len, const void* work, uint32_t nwork,
-                              hipStream_t st)
+                              const uint32_t* seg_len, const void* work, uint32_t ulen,
+                              uint32_t nwork, hipStream_t st)
 {
     switch (k) {
-#define DRAID_CASE(K)                                                                          \
-    case K:                                                                                    \
-        return m == 1 ? go_encode_work<K, 1, CfgDefault<enc_unroll(K)>>(table, k, seg_len, work, \
-                                                                        nwork, st)            \
-                      : go_encode_work<K, 2, CfgDefault<enc_unroll(K)>>(table, k, seg_len, work, \
-                                                                        nwork, st);
+#define DRAID_CASE(K)                                                                        \
+    case K:                                                                                  \
+        return m == 1 ? go_encode_work<K, 1, CfgDefault<enc_unroll(K)>>(table, k, seg_len,   \
+                                                                        work, ulen, nwork, st) \
+                      : go_encode_work<K, 2, CfgDefault<enc_unroll(K)>>(table, k, seg_len,   \
+                                                                        work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return m == 1 ? go_encode_work<0, 1, CfgDefault<2>>(table, k, seg_len, work, nwork, st)
-                      : go_encode_work<0, 2, CfgDefault<2>>(table, k, seg_len, work, nwork, st);
+        return m == 1
+                   ? go_encode_work<0, 1, CfgDefault<2>>(table, k, seg_len, work, ulen, nwork, st)
+                   : go_encode_work<0, 2, CfgDefault<2>>(table, k, seg_len, work, ulen, nwork, st);
     }
 }
 
 hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
                                    const uint32_t* seg_len, const uint8_t* fail, const void* work,
-                                   uint32_t nwork, hipStream_t st)
+                                   uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
     switch (k) {
 #define DRAID_CASE(K)                                                                         \
     case K:                                                                                   \
         return m == 1 ? go_reconstruct_work<K, 1, CfgDefault<rec_unroll(K)>>(                 \
-                            table, k, seg_len, fail, work, nwork, st)                        \
+                            table, k, seg_len, fail, work, ulen, nwork, st)                  \
                       : go_reconstruct_work<K, 2, CfgDefault<rec_unroll(K)>>(                 \
-                            table, k, seg_len, fail, work, nwork, st);
+                            table, k, seg_len, fail, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return m == 1
-                   ? go_reconstruct_work<0, 1, CfgDefault<2>>(table, k, seg_len, fail, work, nwork, st)
-                   : go_reconstruct_work<0, 2, CfgDefault<2>>(table, k, seg_len, fail, work, nwork, st);
+        return m == 1 ? go_reconstruct_work<0, 1, CfgDefault<2>>(table, k, seg_len, fail, work,
+                                                                 ulen, nwork, st)
+                      : go_reconstruct_work<0, 2, CfgDefault<2>>(table, k, seg_len, fail, work,
+                                                                 ulen, nwork, st);
     }
 }
 
 hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* table,
                               const uint8_t* exps, const uint32_t* seg_len, const void* work,
-                              uint32_t nwork, hipStream_t st)
+                              uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
     using C = CfgDefault<1>;
     if (nwork == 0)
         return hipSuccess;
+    const WorkSrc ws = work_src<C>(seg_len, work, ulen);
     if (m == 1)
         hipLaunchKernelGGL((k_update_work<1, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
-                           exps, seg_len, static_cast<const WorkItem*>(work), nwork);
+                           exps, ws, nwork);
     else
         hipLaunchKernelGGL((k_update_work<2, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
-                           exps, seg_len, static_cast<const WorkItem*>(work), nwork);
+                           exps, ws, nwork);
     return hipGetLastError();
 }
 

@@ -51,18 +51,21 @@ hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t
 // 2 read-modify-write update.
 // A work item is {segment, chunk}; chunk covers work_chunk_bytes(op, k) bytes.
 uint32_t work_chunk_bytes(int op, uint32_t k);
+// work == nullptr: every segment is `ulen` bytes and item b is chunk
+// b % cps of segment b / cps (cps = ceil(ulen / work_chunk_bytes)); seg_len
+// is then unused.
 hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,
-                              const uint32_t* seg_len, const void* work, uint32_t nwork,
-                              hipStream_t stream);
+                              const uint32_t* seg_len, const void* work, uint32_t ulen,
+                              uint32_t nwork, hipStream_t stream);
 hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
                                    const uint32_t* seg_len, const uint8_t* fail, const void* work,
-                                   uint32_t nwork, hipStream_t stream);
+                                   uint32_t ulen, uint32_t nwork, hipStream_t stream);
 
 // Read-modify-write parity update over a segment work list (op 2): table rows
 // [O_0, N_0, ..., O_{nd-1}, N_{nd-1}, P, (Q)], exps rows sorted descending.
 hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* table,
                               const uint8_t* exps, const uint32_t* seg_len, const void* work,
-                              uint32_t nwork, hipStream_t stream);
+                              uint32_t ulen, uint32_t nwork, hipStream_t stream);
 
 // Error reporting shared by every C entry point (ec_api.cpp): records the
 // message for draid_ec_last_error(); fail_hip returns -hipError, fail_arg 1.

@@ -1,0 +1,8 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+make -s -C tools/c
+timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+rm -f gpurun_out/sg_bench.log
+for iov in 65536 4096; do timeout -k 10 120 tools/c/sg_bench $iov 4096 10 >> gpurun_out/sg_bench.log 2>&1 || exit 1; done
+cat gpurun_out/sg_bench.log
