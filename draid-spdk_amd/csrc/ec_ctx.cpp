@@ -7,10 +7,11 @@
 //   raid5_chunk_map_iov raid5.c:358-426 (slicing a parent bdev_io's iovecs)
 // Here the same walk runs on the host but, instead of calling the arithmetic per
 // run, it appends each run to a gather-descriptor list (k+m device-accessible
-// pointers + a length).  draid_ec_ctx_flush() uploads every queued descriptor
-// with one DMA from a pinned ring slot and launches one kernel per (op, k, m)
-// group over all of them.  A context is single-threaded, like an SPDK
-// io_channel: one per reactor thread.
+// pointers + a length).  draid_ec_ctx_flush() packs the queued descriptors of
+// each (op, k, m) group into pinned ring slots (about 1 MiB per piece), DMAs
+// each piece on a copy stream and launches one kernel per piece on the compute
+// stream, so uploads overlap kernels.  A context is single-threaded, like an
+// SPDK io_channel: one per reactor thread.
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -25,7 +26,9 @@
 
 namespace {
 
-constexpr int kSlots = 4;
+constexpr int kSlots = 8;
+constexpr size_t kPieceBytes = 1u << 20;       // descriptors per launch (≈ 1 MiB)
+constexpr size_t kMinPieceSegments = 4096;
 constexpr uint64_t kMaxSegment = 1ull << 30;
 
 struct Group {
@@ -40,7 +43,8 @@ struct Slot {
     void* host = nullptr;  // pinned
     void* dev = nullptr;
     size_t cap = 0;
-    hipEvent_t done = nullptr;
+    hipEvent_t done = nullptr;      // the piece's kernel finished (slot reusable)
+    hipEvent_t uploaded = nullptr;  // the piece's descriptors are on the device
     bool used = false;
 };
 
@@ -52,7 +56,8 @@ size_t align8(size_t x) { return (x + 7) & ~size_t(7); }
 }  // namespace
 
 struct draid_ec_ctx {
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // kernels
+    hipStream_t copy = nullptr;     // descriptor uploads
     int device = 0;
     std::vector<Group> groups;
     Slot slots[kSlots];
@@ -125,17 +130,37 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     while (remaining > 0) {
         size_t run = std::min<size_t>(remaining, kMaxSegment);
         for (uint32_t j = 0; j < n; ++j) {
-            while (it[j].idx < it[j].cnt && it[j].off == it[j].v[it[j].idx].iov_len) {
-                ++it[j].idx;  // skip exhausted / zero-length entries
-                it[j].off = 0;
+            IovIter& t = it[j];
+            while (t.idx < t.cnt && t.off == t.v[t.idx].iov_len) {
+                ++t.idx;  // skip exhausted / zero-length entries
+                t.off = 0;
             }
-            if (it[j].idx >= it[j].cnt)
+            if (t.idx >= t.cnt)
                 return rollback("iovec list shorter than len");
-            run = std::min<size_t>(run, it[j].v[it[j].idx].iov_len - it[j].off);
+            // Bytes available contiguously from here: the rest of this iovec plus
+            // any following iovecs that continue it in memory (a split buffer
+            // needs no extra descriptors; the arithmetic is per byte, so merging
+            // adjacent runs cannot change the result).
+            size_t avail = t.v[t.idx].iov_len - t.off;
+            const uint8_t* end = static_cast<const uint8_t*>(t.v[t.idx].iov_base) + t.v[t.idx].iov_len;
+            for (int x = t.idx + 1; x < t.cnt && avail < run; ++x) {
+                if (t.v[x].iov_len == 0)
+                    continue;
+                if (t.v[x].iov_base != end)
+                    break;
+                avail += t.v[x].iov_len;
+                end += t.v[x].iov_len;
+            }
+            run = std::min<size_t>(run, avail);
         }
         for (uint32_t j = 0; j < n; ++j) {
-            g.ptrs.push_back(static_cast<const uint8_t*>(it[j].v[it[j].idx].iov_base) + it[j].off);
-            it[j].off += run;
+            IovIter& t = it[j];
+            g.ptrs.push_back(static_cast<const uint8_t*>(t.v[t.idx].iov_base) + t.off);
+            t.off += run;
+            while (t.idx < t.cnt && t.off > t.v[t.idx].iov_len) {  // crossed merged iovecs
+                t.off -= t.v[t.idx].iov_len;
+                ++t.idx;
+            }
         }
         g.len.push_back(static_cast<uint32_t>(run));
         g.fail.insert(g.fail.end(), meta, meta + nmeta);
@@ -145,23 +170,28 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     return 0;
 }
 
-int flush_group(draid_ec_ctx* c, Group& g)
+// One launch over segments [s0, s1) of a group: pack their descriptors into the
+// next pinned ring slot, DMA them on the copy stream, and launch on the compute
+// stream once the copy has landed.  Copies therefore overlap the kernels of
+// earlier pieces and flushes.
+int flush_piece(draid_ec_ctx* c, const Group& g, size_t s0, size_t s1)
 {
-    const size_t nseg = g.len.size();
-    if (nseg == 0)
-        return 0;
+    const size_t nseg = s1 - s0;
+    const uint32_t n = g.k + g.m;
+    const size_t nmeta = g.fail.size() / g.len.size();  // bytes of meta per segment
     const uint32_t cb = draid::work_chunk_bytes(g.op, g.k);
+    const uint32_t* lenp = g.len.data() + s0;
     // Uniform segments (every run the same length: whole strips, fixed-size
     // iovecs) need no work list -- the kernel derives (segment, chunk) itself.
-    const bool uniform = std::all_of(g.len.begin(), g.len.end(),
-                                     [&](uint32_t l) { return l == g.len[0]; });
+    const bool uniform =
+        std::all_of(lenp, lenp + nseg, [&](uint32_t l) { return l == lenp[0]; });
     std::vector<uint32_t> work;  // pairs {seg, chunk}
     uint64_t nwork64;
     if (uniform) {
-        nwork64 = static_cast<uint64_t>(nseg) * std::max<uint32_t>(1, (g.len[0] + cb - 1) / cb);
+        nwork64 = static_cast<uint64_t>(nseg) * std::max<uint32_t>(1, (lenp[0] + cb - 1) / cb);
     } else {
         for (size_t s = 0; s < nseg; ++s) {
-            const uint32_t cps = std::max<uint32_t>(1, (g.len[s] + cb - 1) / cb);
+            const uint32_t cps = std::max<uint32_t>(1, (lenp[s] + cb - 1) / cb);
             for (uint32_t ch = 0; ch < cps; ++ch) {
                 work.push_back(static_cast<uint32_t>(s));
                 work.push_back(ch);
@@ -173,9 +203,9 @@ int flush_group(draid_ec_ctx* c, Group& g)
         return ctx_arg("flush: too many work items queued (flush more often)");
     const uint32_t nwork = static_cast<uint32_t>(nwork64);
     const size_t o_ptr = 0;
-    const size_t o_len = align8(o_ptr + g.ptrs.size() * sizeof(void*));
+    const size_t o_len = align8(o_ptr + nseg * n * sizeof(void*));
     const size_t o_fail = align8(o_len + (uniform ? 0 : nseg * sizeof(uint32_t)));
-    const size_t o_work = align8(o_fail + g.fail.size());
+    const size_t o_work = align8(o_fail + nseg * nmeta);
     const size_t bytes = o_work + work.size() * sizeof(uint32_t);
 
     Slot& sl = c->slots[c->next];
@@ -201,21 +231,27 @@ int flush_group(draid_ec_ctx* c, Group& g)
         sl.cap = cap;
     }
     uint8_t* h = static_cast<uint8_t*>(sl.host);
-    memcpy(h + o_ptr, g.ptrs.data(), g.ptrs.size() * sizeof(void*));
+    memcpy(h + o_ptr, g.ptrs.data() + s0 * n, nseg * n * sizeof(void*));
     if (!uniform)
-        memcpy(h + o_len, g.len.data(), nseg * sizeof(uint32_t));
-    if (!g.fail.empty())
-        memcpy(h + o_fail, g.fail.data(), g.fail.size());
+        memcpy(h + o_len, lenp, nseg * sizeof(uint32_t));
+    if (nmeta)
+        memcpy(h + o_fail, g.fail.data() + s0 * nmeta, nseg * nmeta);
     if (!work.empty())
         memcpy(h + o_work, work.data(), work.size() * sizeof(uint32_t));
-    if ((e = hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, c->stream)) !=
+    // One DMA of the piece's descriptors.  (Reading them in place from the pinned
+    // slot instead was measured slower: 1.39 vs 1.00 ms for 4096 stripes of 4 KiB
+    // iovecs -- the per-item pointer loads then pay PCIe latency.)
+    if ((e = hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, c->copy)) !=
         hipSuccess)
         return ctx_fail(e, "hipMemcpyAsync(descriptors)");
+    if ((e = hipEventRecord(sl.uploaded, c->copy)) != hipSuccess ||
+        (e = hipStreamWaitEvent(c->stream, sl.uploaded, 0)) != hipSuccess)
+        return ctx_fail(e, "descriptor upload event");
     const uint8_t* d = static_cast<const uint8_t*>(sl.dev);
     const auto* tab = reinterpret_cast<const uint8_t* const*>(d + o_ptr);
     const auto* lens = reinterpret_cast<const uint32_t*>(d + o_len);
     const void* wl = uniform ? nullptr : d + o_work;
-    const uint32_t ulen = g.len[0];
+    const uint32_t ulen = lenp[0];
     if (g.op == 0)
         e = draid::launch_encode_work(g.k, g.m, tab, lens, wl, ulen, nwork, c->stream);
     else if (g.op == 1)
@@ -229,10 +265,25 @@ int flush_group(draid_ec_ctx* c, Group& g)
     if ((e = hipEventRecord(sl.done, c->stream)) != hipSuccess)
         return ctx_fail(e, "hipEventRecord(slot)");
     sl.used = true;
+    return 0;
+}
+
+// Launches a group in pieces of about kPieceBytes of descriptors, so the upload
+// of piece i+1 overlaps the kernel of piece i.
+int flush_group(draid_ec_ctx* c, Group& g)
+{
+    const size_t nseg = g.len.size();
+    if (nseg == 0)
+        return 0;
+    const size_t per_seg = (g.k + g.m) * sizeof(void*) + sizeof(uint32_t) + 2 * sizeof(uint32_t);
+    const size_t piece = std::max<size_t>(kMinPieceSegments, kPieceBytes / per_seg);
+    int rc = 0;
+    for (size_t s0 = 0; s0 < nseg && rc == 0; s0 += piece)
+        rc = flush_piece(c, g, s0, std::min(nseg, s0 + piece));
     g.ptrs.clear();
     g.len.clear();
     g.fail.clear();
-    return 0;
+    return rc;
 }
 
 }  // namespace
@@ -249,8 +300,13 @@ int draid_ec_ctx_create(draid_ec_ctx** out)
     hipError_t e = hipGetDevice(&c->device);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    for (int i = 0; e == hipSuccess && i < kSlots; ++i)
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+    for (int i = 0; e == hipSuccess && i < kSlots; ++i) {
         e = hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming);
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(&c->slots[i].uploaded, hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
         int rc = ctx_fail(e, "draid_ec_ctx_create");
         draid_ec_ctx_destroy(c);
@@ -266,6 +322,8 @@ int draid_ec_ctx_destroy(draid_ec_ctx* c)
         return 0;
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
+    if (c->copy)
+        (void)hipStreamSynchronize(c->copy);
     for (Slot& s : c->slots) {
         if (s.host)
             (void)hipHostFree(s.host);
@@ -273,9 +331,13 @@ int draid_ec_ctx_destroy(draid_ec_ctx* c)
             (void)hipFree(s.dev);
         if (s.done)
             (void)hipEventDestroy(s.done);
+        if (s.uploaded)
+            (void)hipEventDestroy(s.uploaded);
     }
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
+    if (c->copy)
+        (void)hipStreamDestroy(c->copy);
     delete c;
     return 0;
 }

@@ -57,14 +57,17 @@ int main(int argc, char **argv)
         CHECK(draid_ec_stream_synchronize(NULL));
         free(h);
     }
-    /* iovec lists: every strip split into niov pieces */
+    /* iovec lists: every strip split into niov pieces, stored in reverse order
+     * inside the strip's region so that no two consecutive iovecs are adjacent
+     * in memory (a truly scattered list; contiguous pieces would be merged) */
     struct iovec *iov = malloc(sizeof(struct iovec) * (size_t)B * N * niov);
     for (uint32_t s = 0; s < B; ++s)
         for (uint32_t j = 0; j < N; ++j)
             for (size_t v = 0; v < niov; ++v) {
                 struct iovec *e = &iov[((size_t)s * N + j) * niov + v];
-                e->iov_base = buf + ((size_t)s * N + j) * S + v * iov_bytes;
-                e->iov_len = (v + 1) * iov_bytes <= S ? iov_bytes : S - v * iov_bytes;
+                const size_t len = (v + 1) * iov_bytes <= S ? iov_bytes : S - v * iov_bytes;
+                e->iov_base = buf + ((size_t)s * N + j) * S + (S - v * iov_bytes - len);
+                e->iov_len = len;
             }
     draid_ec_ctx *ctx;
     CHECK(draid_ec_ctx_create(&ctx));
@@ -79,7 +82,7 @@ int main(int argc, char **argv)
     for (int op = 0; op < 3; ++op) {
         double walk = 0, flush = 0, wall = 0;
         float gpu = 0;
-        for (int r = -2; r < reps; ++r) { /* two warm-ups */
+        for (int r = -8; r < reps; ++r) { /* warm-ups fill all 8 descriptor slots */
             CHECK(draid_ec_ctx_synchronize(ctx));
             double t0 = now();
             for (uint32_t s = 0; s < B; ++s) {
