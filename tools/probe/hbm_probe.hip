@@ -64,12 +64,12 @@ int probe_copy(const void* src, void* dst, uint64_t bytes, int grid, void* strea
 // the M strips after the data (M = 0: pure read, result stored only if it is an
 // impossible value).
 template <int KT>
-__global__ __launch_bounds__(256) void k_stripe_pattern(uint8_t* base, uint64_t S,
+__global__ __launch_bounds__(64) void k_stripe_pattern(uint8_t* base, uint64_t S,
                                                         uint64_t stripe_stride, int K, int M,
                                                         uint32_t cps, u32x4* sink)
 {
     const uint32_t s = blockIdx.x / cps, c = blockIdx.x % cps;
-    uint8_t* st = base + s * stripe_stride + (uint64_t)c * 4096 + threadIdx.x * 16;
+    uint8_t* st = base + s * stripe_stride + (uint64_t)c * 1024 + threadIdx.x * 16;
     u32x4 acc = 0;
     if constexpr (KT > 0) {
         u32x4 v[KT];
@@ -93,12 +93,13 @@ __global__ __launch_bounds__(256) void k_stripe_pattern(uint8_t* base, uint64_t 
         __builtin_nontemporal_store(acc, (u32x4*)(st + (K + j) * S));
 }
 
-extern "C" int probe_stripe_pattern(void* base, uint64_t S, uint64_t stripe_stride, int K, int M,
-                                    uint32_t nstripes, void* sink, void* stream)
+extern "C" int probe_stripe_pattern(void* base, uint64_t len, uint64_t S, uint64_t stripe_stride,
+                                    int K, int M, uint32_t nstripes, void* sink, void* stream)
 {
-    const uint32_t cps = (uint32_t)(S / 4096);
+    // S = strip stride (len + pad); one wave per 1 KiB chunk of len, as the engine
+    const uint32_t cps = (uint32_t)(len / 1024);
     auto kern = K == 8 ? k_stripe_pattern<8> : K == 16 ? k_stripe_pattern<16> : k_stripe_pattern<0>;
-    hipLaunchKernelGGL(kern, dim3(cps * nstripes), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(kern, dim3(cps * nstripes), dim3(64), 0, (hipStream_t)stream,
                        (uint8_t*)base, S, stripe_stride, K, M, cps, (u32x4*)sink);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

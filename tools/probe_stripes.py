@@ -14,16 +14,18 @@ dev = torch.device("cuda", 0)
 st = torch.cuda.current_stream(dev)
 sink = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
 res = []
-for (K, M, S_kib, B, gap_kib) in [(8, 2, 64, 4096, 0), (8, 2, 128, 2048, 0), (8, 2, 128, 4096, 0),
+CASES = os.environ.get("PROBE_CASES")
+for (K, M, S_kib, B, gap_kib) in (json.loads(CASES) if CASES else [(8, 2, 64, 4096, 0), (8, 2, 128, 2048, 0), (8, 2, 128, 4096, 0),
                                   (8, 2, 256, 1024, 0), (16, 2, 64, 2048, 0), (16, 2, 256, 512, 0),
                                   (8, 2, 128, 4096, 4), (16, 2, 256, 512, 4), (8, 0, 64, 4096, 0),
                                   (8, 0, 128, 4096, 0), (16, 0, 256, 512, 0), (8, 2, 32, 8192, 0),
-                                  (8, 2, 16, 16384, 0)]:
+                                  (8, 2, 16, 16384, 0)]):
     S = S_kib * 1024
-    stride = S + gap_kib * 1024
+    stride = S + int(gap_kib * 1024)
     buf = torch.empty(B * (K + max(M, 2)) * stride + (1 << 20), dtype=torch.uint8, device=dev)
     buf.random_(0, 256)
-    fn = lambda: L.probe_stripe_pattern(C.c_void_p(buf.data_ptr()), C.c_uint64(stride),  # noqa
+    fn = lambda: L.probe_stripe_pattern(C.c_void_p(buf.data_ptr()), C.c_uint64(S),  # noqa
+                                        C.c_uint64(stride),
                                         C.c_uint64((K + max(M, 2)) * stride), K, M, B,
                                         C.c_void_p(sink.data_ptr()), C.c_void_p(st.cuda_stream))
     ts = []
