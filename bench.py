@@ -110,23 +110,33 @@ def load_pmc(workload: str):
 
 
 def cpu_baseline(k: int, m: int, S: int, failures: str, seconds: float, threads: int) -> dict:
-    """The C oracle (isa-l v2.30 restatement, oracle/) timed on the host cores on
-    a bounded sample of the same workload: 64 stripes, encode + reconstruct."""
+    """The CPU restatement of isa-l (oracle/) timed on the host cores on a bounded
+    sample of the same workload: 64 stripes, encode + reconstruct.  Uses the
+    AVX-512 (+GFNI affine) restatement of isa-l's x86 kernels when the host has
+    them (oracle/isal_simd.c), else the scalar one; also times one core."""
     import oracle
     B = 64
     buf = np.frombuffer(np.random.default_rng(1).bytes((k + m) * S * B), np.uint8).copy()
     fail = (failure_pairs if failures == "dual" else failure_single)(B, k, 7).reshape(-1)
-    el, passes = oracle.bench_encode_reconstruct(buf, k, m, S, B, S, (k + m) * S, fail, True,
-                                                 threads, seconds)
-    if el <= 0:
+    simd = oracle.simd_available()
+
+    def run(nthr, secs):
+        el, passes = oracle.bench_encode_reconstruct(buf, k, m, S, B, S, (k + m) * S, fail, True,
+                                                     nthr, secs, simd=simd)
+        return (2.0 * k * S * B * passes / el / GIB, passes, el) if el > 0 else (None, 0, el)
+
+    value, passes, el = run(threads, seconds)
+    if value is None:
         return {"value": None, "error": "oracle bench failed"}
-    user = 2.0 * k * S * B * passes
-    return {"value": round(user / el / GIB, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "port",
+    one, _, _ = run(1, max(1.0, seconds / 4))
+    impl = ("AVX-512BW + GFNI restatement of isa-l's pq_gen_avx512 / gf_vect_mul (affine "
+            "constant multiply)" if simd else
+            "64-bit SWAR restatement of isa-l pq_gen_base + nibble-table gf_vect_mul, -O3 -mavx2")
+    return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "single_core_value": round(one, 3) if one else None,
             "sample": f"{B} stripes x {k}+{m} x {S // 1024} KiB, encode + {failures}-failure "
-                      f"reconstruct, {passes} passes in {el:.1f}s, C oracle (64-bit SWAR "
-                      f"restatement of isa-l pq_gen_base + nibble-table gf_vect_mul), "
-                      f"-O3 -mavx2, {threads} pthreads"}
+                      f"reconstruct, {passes} passes in {el:.1f}s, C oracle ({impl}), "
+                      f"{threads} pthreads"}
 
 
 def main() -> None:

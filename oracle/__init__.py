@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(HERE, f) for f in ("isal_oracle.c", "bdevperf_raid5.c", "isal_oracle.h")]
+    srcs = [os.path.join(HERE, f) for f in ("isal_oracle.c", "isal_simd.c", "bdevperf_raid5.c", "isal_oracle.h")]
     if force or not os.path.exists(LIB_PATH) or \
             os.path.getmtime(LIB_PATH) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
@@ -53,6 +53,12 @@ def lib() -> C.CDLL:
         L.orc_bench_encode_reconstruct.restype = C.c_double
         L.orc_bench_encode_reconstruct.argtypes = [i32, i32, sz, u32, vp, sz, sz, vp, i32, i32,
                                                    C.c_double, C.POINTER(C.c_uint64)]
+        L.orc_bench_encode_reconstruct_impl.restype = C.c_double
+        L.orc_bench_encode_reconstruct_impl.argtypes = [i32, i32, i32, sz, u32, vp, sz, sz, vp,
+                                                        i32, i32, C.c_double,
+                                                        C.POINTER(C.c_uint64)]
+        L.orc_simd_encode_strided.argtypes = [i32, i32, sz, u32, vp, sz, sz]
+        L.orc_simd_recover_strided.argtypes = [i32, i32, sz, u32, vp, sz, sz, vp]
         L.orc_raid5_parity_chunk.argtypes = [i32, i32, C.c_uint64]
         L.orc_raid5_data_chunk_to_disk.argtypes = [i32, i32]
         P64 = C.POINTER(C.c_uint64)
@@ -185,15 +191,34 @@ def ut_ref_pattern(num_blocks: int, blocklen: int) -> np.ndarray:
     return b
 
 
+def simd_available() -> bool:
+    return bool(lib().orc_simd_available())
+
+
+def simd_encode_strided(buf: np.ndarray, k: int, m: int, length: int, nstripes: int,
+                        strip_stride: int, stripe_stride: int) -> int:
+    return lib().orc_simd_encode_strided(k, m, length, nstripes, buf.ctypes.data, strip_stride,
+                                         stripe_stride)
+
+
+def simd_recover_strided(buf: np.ndarray, k: int, m: int, length: int, nstripes: int,
+                         strip_stride: int, stripe_stride: int, fail: np.ndarray) -> int:
+    fail = np.ascontiguousarray(fail, dtype=np.uint8)
+    return lib().orc_simd_recover_strided(k, m, length, nstripes, buf.ctypes.data, strip_stride,
+                                          stripe_stride, fail.ctypes.data)
+
+
 def bench_encode_reconstruct(buf: np.ndarray, k: int, m: int, length: int, nstripes: int,
                              strip_stride: int, stripe_stride: int, fail: np.ndarray,
-                             with_reconstruct: bool, nthreads: int, min_seconds: float):
+                             with_reconstruct: bool, nthreads: int, min_seconds: float,
+                             simd: bool = False):
+    """Times the scalar restatement (simd=False) or the AVX-512 one (simd=True)."""
     passes = C.c_uint64()
     fail = np.ascontiguousarray(fail, dtype=np.uint8)
-    el = lib().orc_bench_encode_reconstruct(k, m, length, nstripes, buf.ctypes.data, strip_stride,
-                                            stripe_stride, fail.ctypes.data,
-                                            int(with_reconstruct), nthreads, min_seconds,
-                                            C.byref(passes))
+    el = lib().orc_bench_encode_reconstruct_impl(int(simd), k, m, length, nstripes,
+                                                 buf.ctypes.data, strip_stride, stripe_stride,
+                                                 fail.ctypes.data, int(with_reconstruct),
+                                                 nthreads, min_seconds, C.byref(passes))
     return el, passes.value
 
 

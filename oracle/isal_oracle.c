@@ -404,7 +404,7 @@ int orc_recover_strided(int k, int m, size_t len, uint32_t nstripes,
 /* ------------------------------------------------------- CPU baseline */
 
 struct bench_arg {
-    int k, m, with_rec;
+    int impl, k, m, with_rec;
     size_t len, strip_stride, stripe_stride;
     uint32_t s0, s1;
     uint8_t *base;
@@ -417,6 +417,14 @@ static void *bench_worker(void *p)
     struct bench_arg *a = p;
     uint32_t n = a->s1 - a->s0;
     uint8_t *b = a->base + (size_t)a->s0 * a->stripe_stride;
+    if (a->impl == 1) {
+        a->rc = orc_simd_encode_strided(a->k, a->m, a->len, n, b, a->strip_stride,
+                                        a->stripe_stride);
+        if (!a->rc && a->with_rec)
+            a->rc = orc_simd_recover_strided(a->k, a->m, a->len, n, b, a->strip_stride,
+                                             a->stripe_stride, a->fail + 2 * (size_t)a->s0);
+        return NULL;
+    }
     a->rc = orc_encode_strided(a->k, a->m, a->len, n, b, a->strip_stride, a->stripe_stride);
     if (!a->rc && a->with_rec)
         a->rc = orc_recover_strided(a->k, a->m, a->len, n, b, a->strip_stride,
@@ -437,6 +445,17 @@ double orc_bench_encode_reconstruct(int k, int m, size_t len, uint32_t nstripes,
                                     int with_reconstruct, int nthreads,
                                     double min_seconds, uint64_t *passes)
 {
+    return orc_bench_encode_reconstruct_impl(0, k, m, len, nstripes, base, strip_stride,
+                                             stripe_stride, fail, with_reconstruct, nthreads,
+                                             min_seconds, passes);
+}
+
+double orc_bench_encode_reconstruct_impl(int impl, int k, int m, size_t len, uint32_t nstripes,
+                                         uint8_t *base, size_t strip_stride,
+                                         size_t stripe_stride, const uint8_t *fail,
+                                         int with_reconstruct, int nthreads,
+                                         double min_seconds, uint64_t *passes)
+{
     if (nthreads < 1)
         nthreads = 1;
     if ((uint32_t)nthreads > nstripes)
@@ -449,7 +468,8 @@ double orc_bench_encode_reconstruct(int k, int m, size_t len, uint32_t nstripes,
         return -1.0;
     }
     for (int t = 0; t < nthreads; t++) {
-        args[t] = (struct bench_arg){ k, m, with_reconstruct, len, strip_stride, stripe_stride,
+        args[t] = (struct bench_arg){ impl, k, m, with_reconstruct, len, strip_stride,
+                                      stripe_stride,
                                       (uint32_t)((uint64_t)nstripes * t / nthreads),
                                       (uint32_t)((uint64_t)nstripes * (t + 1) / nthreads),
                                       base, fail, 0 };

@@ -61,6 +61,21 @@ int orc_recover_strided(int k, int m, size_t len, uint32_t nstripes,
  * with_reconstruct) over the strided batch for at least min_seconds using
  * nthreads pthreads (stripes partitioned by contiguous ranges).  Returns the
  * elapsed seconds and writes the number of full passes done to *passes. */
+/* AVX-512 (+GFNI affine) restatement of isa-l's x86 kernels (isal_simd.c):
+ * the CPU baseline.  Same results and failure semantics as the strided calls
+ * above, except that unrecoverable / empty failure sets are skipped (as the
+ * GPU kernels do).  -1 when the CPU lacks AVX-512BW or GFNI. */
+int orc_simd_available(void);
+int orc_simd_encode_strided(int k, int m, size_t len, uint32_t nstripes, uint8_t *base,
+                            size_t strip_stride, size_t stripe_stride);
+int orc_simd_recover_strided(int k, int m, size_t len, uint32_t nstripes, uint8_t *base,
+                             size_t strip_stride, size_t stripe_stride, const uint8_t *fail);
+/* impl 0: scalar restatement, 1: AVX-512 restatement */
+double orc_bench_encode_reconstruct_impl(int impl, int k, int m, size_t len, uint32_t nstripes,
+                                         uint8_t *base, size_t strip_stride,
+                                         size_t stripe_stride, const uint8_t *fail,
+                                         int with_reconstruct, int nthreads,
+                                         double min_seconds, uint64_t *passes);
 double orc_bench_encode_reconstruct(int k, int m, size_t len, uint32_t nstripes,
                                     uint8_t *base, size_t strip_stride,
                                     size_t stripe_stride, const uint8_t *fail,

@@ -199,3 +199,48 @@ def test_sg_uniform_segments(ec, L, piece):
         assert (buf.cpu().numpy() == ref).all()
     finally:
         ctx.close()
+
+
+def test_sg_adjacent_iovecs_merge(ec):
+    """Memory-contiguous iovecs (and zero-length ones between them) are walked as
+    one run: a strip split into adjacent pieces queues a single segment, the same
+    split with gaps between the pieces queues one per piece, and both encode the
+    same parity (the oracle's)."""
+    k, m, L = 4, 2, 8192
+    n = k + m
+    cuts = [0, 1000, 1000, 4096, 5000, L]   # includes a zero-length piece
+    pieces = [(a, b - a) for a, b in zip(cuts, cuts[1:])]
+    gap = 64
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    buf = torch.randint(0, 256, (n, L), dtype=torch.uint8, device=DEV, generator=g)
+    buf[k:] = 0
+    # the same strips scattered: piece i of strip j at j*(L+5*gap) + a + i*gap
+    sc = torch.zeros(n * (L + 5 * gap), dtype=torch.uint8, device=DEV)
+    for j in range(n):
+        for i, (a, ln) in enumerate(pieces):
+            o = j * (L + 5 * gap) + a + i * gap
+            sc[o:o + ln] = buf[j, a:a + ln]
+    bb, sb = buf.data_ptr(), sc.data_ptr()
+    ctx = ec.Ctx()
+    try:
+        assert ctx.encode_sg(k, m, [[(bb + j * L + a, ln) for a, ln in pieces]
+                                    for j in range(n)], L) == 0
+        assert ctx.queued() == 1
+        assert ctx.encode_sg(k, m, [[(sb + j * (L + 5 * gap) + a + i * gap, ln)
+                                     for i, (a, ln) in enumerate(pieces)]
+                                    for j in range(n)], L) == 0
+        assert ctx.queued() == 1 + sum(1 for _, ln in pieces if ln)
+        ctx.flush()
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    got = buf.cpu().numpy()
+    ref = got.copy()
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, 1, L, n * L) == 0
+    assert (got == ref).all()
+    scat = sc.cpu().numpy()
+    for j in range(k, n):
+        strip = np.concatenate([scat[j * (L + 5 * gap) + a + i * gap:][:ln]
+                                for i, (a, ln) in enumerate(pieces)])
+        assert (strip == ref[j]).all()

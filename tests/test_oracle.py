@@ -236,3 +236,32 @@ def test_bench_sample_runs():
     fail[1::2] = 6
     el, passes = oracle.bench_encode_reconstruct(buf, k, m, L, B, L, (k + m) * L, fail, True, 2, 0.01)
     assert el > 0 and passes >= 1
+
+
+@pytest.mark.skipif(not oracle.simd_available(), reason="CPU lacks AVX-512BW/GFNI")
+@pytest.mark.parametrize("k,m,L", [(1, 2, 200), (2, 1, 64), (4, 1, 4096 + 7), (8, 2, 65536),
+                                   (14, 2, 4096), (16, 2, 1000), (3, 2, 129)])
+def test_simd_matches_scalar(k, m, L):
+    """The AVX-512 restatement (the bench's CPU baseline) is byte-exact with the
+    scalar oracle for encode and for every single/double failure set."""
+    n = k + m
+    pairs = [(x, 0xFF) for x in range(n)]
+    if m == 2:
+        pairs += [(x, y) for x in range(n) for y in range(n) if x != y]
+    B = len(pairs)
+    rng = np.random.default_rng(k * 100 + L)
+    buf = np.zeros((B, n, L), np.uint8)
+    buf[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    ref = buf.copy()
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, B, L, n * L) == 0
+    got = buf.copy()
+    assert oracle.simd_encode_strided(got.reshape(-1), k, m, L, B, L, n * L) == 0
+    assert (got == ref).all()
+    fail = np.array(pairs, np.uint8)
+    for s, (x, y) in enumerate(pairs):
+        got[s, x] = 0x5A
+        if y != 0xFF:
+            got[s, y] = 0xA5
+    assert oracle.simd_recover_strided(got.reshape(-1), k, m, L, B, L, n * L,
+                                       fail.reshape(-1)) == 0
+    assert (got == ref).all()
