@@ -450,6 +450,41 @@ double orc_bench_encode_reconstruct(int k, int m, size_t len, uint32_t nstripes,
                                              min_seconds, passes);
 }
 
+/* Persistent workers: every thread runs its stripe range once per pass, then
+ * meets the others at a barrier, where thread 0 decides whether to stop (thread
+ * creation per pass would dominate short passes). */
+struct bench_team {
+    struct bench_arg *args;
+    pthread_barrier_t bar;
+    double t0, min_seconds, el;
+    uint64_t passes;
+    volatile int stop;
+};
+
+struct bench_thread {
+    struct bench_team *team;
+    int id;
+};
+
+static void *bench_loop(void *p)
+{
+    struct bench_thread *bt = p;
+    struct bench_team *tm = bt->team;
+    for (;;) {
+        bench_worker(&tm->args[bt->id]);
+        pthread_barrier_wait(&tm->bar);
+        if (bt->id == 0) {
+            tm->passes++;
+            tm->el = now_s() - tm->t0;
+            tm->stop = tm->el >= tm->min_seconds;
+        }
+        pthread_barrier_wait(&tm->bar);
+        if (tm->stop)
+            break;
+    }
+    return NULL;
+}
+
 double orc_bench_encode_reconstruct_impl(int impl, int k, int m, size_t len, uint32_t nstripes,
                                          uint8_t *base, size_t strip_stride,
                                          size_t stripe_stride, const uint8_t *fail,
@@ -461,10 +496,13 @@ double orc_bench_encode_reconstruct_impl(int impl, int k, int m, size_t len, uin
     if ((uint32_t)nthreads > nstripes)
         nthreads = (int)nstripes;
     struct bench_arg *args = calloc((size_t)nthreads, sizeof(*args));
+    struct bench_thread *bt = calloc((size_t)nthreads, sizeof(*bt));
     pthread_t *th = calloc((size_t)nthreads, sizeof(*th));
-    if (!args || !th) {
+    struct bench_team tm;
+    if (!args || !th || !bt || pthread_barrier_init(&tm.bar, NULL, (unsigned)nthreads)) {
         free(args);
         free(th);
+        free(bt);
         return -1.0;
     }
     for (int t = 0; t < nthreads; t++) {
@@ -473,25 +511,29 @@ double orc_bench_encode_reconstruct_impl(int impl, int k, int m, size_t len, uin
                                       (uint32_t)((uint64_t)nstripes * t / nthreads),
                                       (uint32_t)((uint64_t)nstripes * (t + 1) / nthreads),
                                       base, fail, 0 };
+        bt[t] = (struct bench_thread){ &tm, t };
     }
-    uint64_t n = 0;
-    double t0 = now_s(), el = 0.0;
-    do {
-        for (int t = 1; t < nthreads; t++)
-            pthread_create(&th[t], NULL, bench_worker, &args[t]);
-        bench_worker(&args[0]);
-        for (int t = 1; t < nthreads; t++)
-            pthread_join(th[t], NULL);
-        n++;
-        el = now_s() - t0;
-    } while (el < min_seconds);
+    tm.args = args;
+    tm.min_seconds = min_seconds;
+    tm.passes = 0;
+    tm.stop = 0;
+    tm.el = 0.0;
+    tm.t0 = now_s();
+    for (int t = 1; t < nthreads; t++)
+        pthread_create(&th[t], NULL, bench_loop, &bt[t]);
+    bench_loop(&bt[0]);
+    for (int t = 1; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&tm.bar);
+    double el = tm.el;
     for (int t = 0; t < nthreads; t++)
         if (args[t].rc)
             el = -1.0;
     free(args);
     free(th);
+    free(bt);
     if (passes)
-        *passes = n;
+        *passes = tm.passes;
     return el;
 }
 
