@@ -869,9 +869,12 @@ using V17 = Cfg<512, 1, 3, 3, 0>;  // XCD-aware, 512 lanes
 using V18 = Cfg<64, 2, 3, 0, 0>;   // one wave, U=2
 using V19 = Cfg<64, 4, 3, 0, 0>;   // one wave, U=4
 using V20 = Cfg<64, 1, 3, 3, 0>;   // one wave, XCD-aware
+using V21 = Cfg<64, 1, 1, 0, 0>;   // one wave, nt loads, plain stores
+using V22 = Cfg<64, 1, 2, 0, 0>;   // one wave, plain loads, nt stores
+using V23 = Cfg<64, 1, 0, 0, 0>;   // one wave, plain loads and stores
 #define DRAID_VARIANTS(X) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5) X(6, V6) X(7, V7) X(8, V8) \
     X(9, V9) X(10, V10) X(11, V11) X(12, V12) X(13, V13) X(14, V14) X(15, V15) X(16, V16)     \
-    X(17, V17) X(18, V18) X(19, V19) X(20, V20)
+    X(17, V17) X(18, V18) X(19, V19) X(20, V20) X(21, V21) X(22, V22) X(23, V23)
 
 template <int K, int M>
 static hipError_t variant_encode(int v, const TablePtrs& pp, uint64_t len, uint32_t ns,

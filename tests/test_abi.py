@@ -4,6 +4,7 @@ call is made (there is no GPU here)."""
 import ctypes
 import os
 import re
+import shutil
 import subprocess
 
 import oracle
@@ -35,9 +36,12 @@ def test_library_exports_header_symbols():
     assert sorted(draid_ec.EXPORTS) == header_functions(draid_ec.HEADER)
 
 
-def test_library_is_gfx950_code_object():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", "-h",
-                          draid_ec.LIB_PATH], capture_output=True, text=True, cwd="/tmp")
+def test_library_is_gfx950_code_object(tmp_path):
+    # --offloading extracts the bundles next to its input: run it on a copy
+    lib = tmp_path / "libdraid_ec.so"
+    shutil.copy(draid_ec.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", "-h", str(lib)],
+                         capture_output=True, text=True, cwd=str(tmp_path))
     blob = out.stdout + out.stderr
     if "gfx" not in blob:  # older objdump: fall back to strings in the bundle
         blob = open(draid_ec.LIB_PATH, "rb").read().decode("latin-1")

@@ -25,7 +25,8 @@ VARIANTS = {0: "default (64 lanes U1)", 1: "U2", 2: "512 lanes U1", 3: "128 lane
             8: "1024 lanes", 9: "64 lanes", 10: "256 lanes U1", 11: "512 lanes U2", 12: "U4",
             13: "DIAG no-plan U2", 14: "DIAG no-plan U1", 15: "DIAG no-plan no-mul U1",
             16: "XCD-aware map", 17: "XCD-aware 512 lanes",
-            18: "64 lanes U2", 19: "64 lanes U4", 20: "64 lanes XCD-aware"}
+            18: "64 lanes U2", 19: "64 lanes U4", 20: "64 lanes XCD-aware",
+            21: "64 lanes nt loads only", 22: "64 lanes nt stores only", 23: "64 lanes no nt"}
 
 
 def probe(torch, dev, nbytes, rounds, iters):
