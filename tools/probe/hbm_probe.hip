@@ -103,3 +103,37 @@ extern "C" int probe_stripe_pattern(void* base, uint64_t len, uint64_t S, uint64
                        (uint8_t*)base, S, stripe_stride, K, M, cps, (u32x4*)sink);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Write-only, one item per workgroup (the engine's shape): workgroup b writes
+// NTHR*VPL*16 contiguous bytes, VPL vectors per lane NTHR apart.
+template <int NTHR, int VPL, bool NT>
+__global__ __launch_bounds__(NTHR) void k_write_items(u32x4* dst)
+{
+    u32x4* p = dst + (uint64_t)blockIdx.x * NTHR * VPL + threadIdx.x;
+    const u32x4 v = (u32x4)(blockIdx.x ^ threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        if constexpr (NT)
+            __builtin_nontemporal_store(v, p + u * NTHR);
+        else
+            p[u * NTHR] = v;
+    }
+}
+
+extern "C" int probe_write_items(void* dst, uint64_t bytes, int nthr, int vpl, int nt, void* stream)
+{
+    const uint64_t per = (uint64_t)nthr * vpl * 16;
+    const dim3 g((unsigned)(bytes / per));
+    hipStream_t s = (hipStream_t)stream;
+#define W(N, V)                                                                      \
+    if (nthr == N && vpl == V) {                                                     \
+        if (nt)                                                                      \
+            hipLaunchKernelGGL((k_write_items<N, V, true>), g, dim3(N), 0, s, (u32x4*)dst);  \
+        else                                                                         \
+            hipLaunchKernelGGL((k_write_items<N, V, false>), g, dim3(N), 0, s, (u32x4*)dst); \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                             \
+    }
+    W(64, 1) W(64, 4) W(256, 1) W(256, 4) W(1024, 1)
+#undef W
+    return -2;
+}
