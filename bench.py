@@ -154,6 +154,9 @@ def main() -> None:
                     help="backend of the timing collectives (nccl = RCCL; gloo only for "
                          "rehearsing several ranks on one GPU)")
     args = ap.parse_args()
+    if args.variant:  # A/B kernel variants exist only in the lab build (tools/sweep.py)
+        os.environ.setdefault("DRAID_EC_LIB",
+                              os.path.join(ROOT, "draid-spdk_amd", "liblab", "libdraid_ec.so"))
 
     import torch
     import torch.distributed as dist

@@ -30,8 +30,12 @@ constexpr uint64_t kMaxStripLen = 0x7fff0000ull;
 
 __constant__ GfTables c_gf = make_gf_tables();
 
+#ifndef DRAID_EC_LAB
+#define DRAID_EC_LAB 0
+#endif
+// Variant selector: only the lab build has variants; the product ignores it.
 static int g_variant = 0;
-void set_variant(int v) { g_variant = v; }
+void set_variant(int v) { g_variant = DRAID_EC_LAB ? v : 0; }
 int get_variant() { return g_variant; }
 
 // ------------------------------------------------------------ pointers
@@ -741,7 +745,7 @@ static inline uint32_t chunks_per_stripe(uint64_t len, int nthr, int U)
     return static_cast<uint32_t>(c == 0 ? 1 : c);
 }
 
-static int device_cus()
+[[maybe_unused]] static int device_cus()
 {
     static thread_local int dev = -1, cus = 0;
     int d = 0;
@@ -848,7 +852,10 @@ static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
     }
 }
 
-// A/B variants of the RAID6 8+2 batched kernels (tools/sweep.py only).
+#if DRAID_EC_LAB
+// A/B variants of the batched kernels at the BASELINE shapes, for tools/sweep.py.
+// Compiled only into the lab build (make lab -> liblab/libdraid_ec.so); the
+// product library carries the production configuration alone.
 using V1 = Cfg<256, 2, 3, 0, 0>;   // U=2
 using V2 = Cfg<512, 1, 3, 0, 0>;   // 512 lanes
 using V3 = Cfg<128, 1, 3, 0, 0>;   // 128 lanes
@@ -911,16 +918,19 @@ static bool has_variants(uint32_t k, uint32_t m)
 {
     return (k == 4 && m == 1) || (k == 8 && m == 2) || (k == 16 && m == 2);
 }
+#endif  // DRAID_EC_LAB
 
 hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
                          const uint8_t* const* table, const ArgPtrTable* args, hipStream_t st)
 {
     if (table) {
         const TablePtrs pp{table, k + m};
+#if DRAID_EC_LAB
         if (g_variant != 0 && has_variants(k, m))
             return k == 4 ? variant_encode<4, 1>(g_variant, pp, len, nstripes, st)
                  : k == 8 ? variant_encode<8, 2>(g_variant, pp, len, nstripes, st)
                           : variant_encode<16, 2>(g_variant, pp, len, nstripes, st);
+#endif
         if (m == 1)
             return dispatch_encode<1>(pp, k, len, nstripes, st);
         return dispatch_encode<2>(pp, k, len, nstripes, st);
@@ -938,10 +948,12 @@ hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nst
     const uint32_t f01 = static_cast<uint32_t>(f0) | (static_cast<uint32_t>(f1) << 8);
     if (table) {
         const TablePtrs pp{table, k + m};
+#if DRAID_EC_LAB
         if (g_variant != 0 && has_variants(k, m) && fail_dev)
             return k == 4 ? variant_reconstruct<4, 1>(g_variant, pp, len, nstripes, fail_dev, st)
                  : k == 8 ? variant_reconstruct<8, 2>(g_variant, pp, len, nstripes, fail_dev, st)
                           : variant_reconstruct<16, 2>(g_variant, pp, len, nstripes, fail_dev, st);
+#endif
         if (m == 1)
             return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, f01, st);
         return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, f01, st);

@@ -12,7 +12,10 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdraid_ec.so")
+# DRAID_EC_LIB selects another build of the same ABI (tools: the lab build with
+# kernel variants, `make -C draid-spdk_amd lab`).
+LIB_PATH = os.environ.get("DRAID_EC_LIB") or os.path.join(HERE, "libdraid_ec.so")
+LAB_LIB_PATH = os.path.join(HERE, "liblab", "libdraid_ec.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "draid_ec.h")
 
 FAIL_NONE = 0xFF
@@ -63,7 +66,8 @@ class DraidError(RuntimeError):
 def build(force: bool = False) -> str:
     """Compile libdraid_ec.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
     if force or not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", HERE, "libdraid_ec.so"])
+        target = "lab" if os.path.abspath(LIB_PATH) == LAB_LIB_PATH else "libdraid_ec.so"
+        subprocess.check_call(["make", "-s", "-C", HERE, target])
     return LIB_PATH
 
 

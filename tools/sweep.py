@@ -19,6 +19,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "draid-spdk_amd"))
 sys.path.insert(0, ROOT)
+# kernel variants live in the lab build of the library only
+os.environ.setdefault("DRAID_EC_LIB",
+                      os.path.join(ROOT, "draid-spdk_amd", "liblab", "libdraid_ec.so"))
 
 VARIANTS = {0: "default (64 lanes U1)", 1: "U2", 2: "512 lanes U1", 3: "128 lanes",
             4: "chunk-major map", 5: "persistent", 6: "scalar plan", 7: "persist 512 scalar",
@@ -26,7 +29,7 @@ VARIANTS = {0: "default (64 lanes U1)", 1: "U2", 2: "512 lanes U1", 3: "128 lane
             13: "DIAG no-plan U2", 14: "DIAG no-plan U1", 15: "DIAG no-plan no-mul U1",
             16: "XCD-aware map", 17: "XCD-aware 512 lanes",
             18: "64 lanes U2", 19: "64 lanes U4", 20: "64 lanes XCD-aware",
-            21: "64 lanes nt loads only", 22: "64 lanes nt stores only", 23: "64 lanes no nt"}
+            21: "64 lanes nt loads only", 22: "64 lanes nt stores only",23: "64 lanes no nt"}
 
 
 def probe(torch, dev, nbytes, rounds, iters):

@@ -1,5 +1,6 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+make -s -C draid-spdk_amd -j8 lab || exit 1
 L=stripe_major,stripe_major_gap4096,stripe_major_gap65536,strip_major
 V=0,1,2,4,10,11,12
 timeout -k 10 300 python tools/sweep.py --k 8 --strip-kib 128 --stripes 4096 --failures single --layouts $L --variants $V --out gpurun_out/sweep_8p2_128k.json > gpurun_out/sw1.log 2>&1 || exit 1
