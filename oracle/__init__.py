@@ -57,6 +57,7 @@ def lib() -> C.CDLL:
         L.orc_bench_encode_reconstruct_impl.argtypes = [i32, i32, i32, sz, u32, vp, sz, sz, vp,
                                                         i32, i32, C.c_double,
                                                         C.POINTER(C.c_uint64)]
+        L.orc_simd_xor_gen.argtypes = [i32, i32, C.POINTER(vp)]
         L.orc_simd_encode_strided.argtypes = [i32, i32, sz, u32, vp, sz, sz]
         L.orc_simd_recover_strided.argtypes = [i32, i32, sz, u32, vp, sz, sz, vp]
         L.orc_raid5_parity_chunk.argtypes = [i32, i32, C.c_uint64]
@@ -193,6 +194,10 @@ def ut_ref_pattern(num_blocks: int, blocklen: int) -> np.ndarray:
 
 def simd_available() -> bool:
     return bool(lib().orc_simd_available())
+
+
+def simd_xor_gen(vects: list[np.ndarray], length: int) -> int:
+    return lib().orc_simd_xor_gen(len(vects), length, _ptrs(vects))
 
 
 def simd_encode_strided(buf: np.ndarray, k: int, m: int, length: int, nstripes: int,

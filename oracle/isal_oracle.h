@@ -66,6 +66,7 @@ int orc_recover_strided(int k, int m, size_t len, uint32_t nstripes,
  * above, except that unrecoverable / empty failure sets are skipped (as the
  * GPU kernels do).  -1 when the CPU lacks AVX-512BW or GFNI. */
 int orc_simd_available(void);
+int orc_simd_xor_gen(int vects, int len, void **array);
 int orc_simd_encode_strided(int k, int m, size_t len, uint32_t nstripes, uint8_t *base,
                             size_t strip_stride, size_t stripe_stride);
 int orc_simd_recover_strided(int k, int m, size_t len, uint32_t nstripes, uint8_t *base,

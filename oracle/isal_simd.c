@@ -169,6 +169,30 @@ SIMD_TARGET static int recover_one(int k, int m, size_t len, unsigned char **v, 
     return 0;
 }
 
+/* xor_gen(vects, len, array) (isa-l raid.h semantics, xor_gen_avx512): the last
+ * pointer receives the XOR of the others; any length (bytewise tail). */
+SIMD_TARGET int orc_simd_xor_gen(int vects, int len, void **array)
+{
+    if (vects < 3 || len < 0)
+        return 1;
+    unsigned char **v = (unsigned char **)array;
+    const int k = vects - 1;
+    const size_t body = (size_t)len & ~(size_t)63;
+    for (size_t i = 0; i < body; i += 64) {
+        __m512i p = ld(v[0] + i);
+        for (int j = 1; j < k; j++)
+            p = _mm512_xor_si512(p, ld(v[j] + i));
+        st(v[k] + i, p);
+    }
+    for (size_t i = body; i < (size_t)len; i++) {
+        unsigned char p = v[0][i];
+        for (int j = 1; j < k; j++)
+            p ^= v[j][i];
+        v[k][i] = p;
+    }
+    return 0;
+}
+
 int orc_simd_encode_strided(int k, int m, size_t len, uint32_t nstripes, uint8_t *base,
                             size_t strip_stride, size_t stripe_stride)
 {

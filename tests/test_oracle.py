@@ -265,3 +265,14 @@ def test_simd_matches_scalar(k, m, L):
     assert oracle.simd_recover_strided(got.reshape(-1), k, m, L, B, L, n * L,
                                        fail.reshape(-1)) == 0
     assert (got == ref).all()
+
+
+@pytest.mark.skipif(not oracle.simd_available(), reason="CPU lacks AVX-512BW/GFNI")
+@pytest.mark.parametrize("vects,L", [(3, 64), (5, 65536), (3, 1), (17, 4096 + 33)])
+def test_simd_xor_gen_matches_scalar(vects, L):
+    rng = np.random.default_rng(vects + L)
+    a = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(vects - 1)] + [np.zeros(L, np.uint8)]
+    b = [x.copy() for x in a]
+    assert oracle.xor_gen(a, L) == 0
+    assert oracle.simd_xor_gen(b, L) == 0
+    assert all((x == y).all() for x, y in zip(a, b))

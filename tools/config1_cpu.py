@@ -28,6 +28,8 @@ def main():
     r = {"config": "RAID5 4+1 full-stripe write, 64 KiB strip, bdevperf-style over 5 RAM disks",
          "io_size": 262144, "cores": 1, "seconds": secs, "ios": ios, "mib_s": round(mibs, 1),
          "iops": round(ios / secs, 1), "parity_verified": ok, "cpu": cpu_model(),
+         "xor_gen": "AVX-512 restatement of isa-l xor_gen_avx512 (oracle/isal_simd.c)"
+         if oracle.simd_available() else "scalar restatement",
          "kind": "port (oracle xor_gen restatement + memcpy per strip)"}
     print(json.dumps(r))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
