@@ -443,3 +443,143 @@ int draid_raid_stripe_write_partial(const struct draid_raid *r, draid_ec_ctx *ct
     *nwrites = nw;
     return 0;
 }
+
+/* ------------------------------------------------------------ ranged reads */
+
+/* One base read of data chunk d's requested blocks into the parent iovecs
+ * (CHUNK_READ, raid5.c:929-930,935-943). */
+static int read_request(const struct draid_raid *r, const struct draid_stripe_req *req, int d,
+                        const struct iovec *iov, int iovcnt, struct draid_base_io *io)
+{
+    const int disk = draid_raid_data_disk(r, req->stripe_index, d);
+    const struct draid_chunk_req *c = &req->chunk[disk];
+    io->disk = disk;
+    io->offset_blocks = (req->stripe_index << r->strip_size_shift) + c->req_offset;
+    io->num_blocks = c->req_blocks;
+    const int cnt = user_slice(r, req, d, c->req_offset, c->req_offset + c->req_blocks, iov,
+                               iovcnt, io->iov, DRAID_RAID_MAX_IOV);
+    if (cnt < 0)
+        return cnt;
+    io->iovcnt = cnt;
+    return 0;
+}
+
+/* The part of strip range [a, b) that data chunk d's request covers, clamped:
+ * [*u0, *u1), or empty (*u0 == *u1 == b) for parity, unrequested chunks and
+ * disjoint requests. */
+static void covered(const struct draid_chunk_req *c, int d, uint64_t a, uint64_t b, uint64_t *u0,
+                    uint64_t *u1)
+{
+    uint64_t x = c->req_offset, y = c->req_offset + c->req_blocks;
+    if (d < 0 || !c->req_blocks || y <= a || x >= b)
+        x = y = b;
+    *u0 = x < a ? a : x;
+    *u1 = y > b ? b : y;
+}
+
+/* Strip j's iovecs over [a, b): the covered part from the parent iovecs, the
+ * rest at the same offset in buf. */
+static int range_list(const struct draid_raid *r, const struct draid_stripe_req *req, int disk,
+                      int d, uint64_t a, uint64_t b, const struct iovec *iov, int iovcnt,
+                      void *buf, struct iovec *out, int out_max)
+{
+    const uint32_t bl = r->blocklen;
+    uint64_t u0, u1;
+    covered(&req->chunk[disk], d, a, b, &u0, &u1);
+    int n = 0;
+    if (a < u0) {
+        out[n].iov_base = (uint8_t *)buf + a * bl;
+        out[n++].iov_len = (u0 - a) * bl;
+    }
+    if (u0 < u1) {
+        const int c2 = user_slice(r, req, d, u0, u1, iov, iovcnt, out + n, out_max - n - 1);
+        if (c2 < 0)
+            return c2;
+        n += c2;
+    }
+    if (u1 < b) {
+        out[n].iov_base = (uint8_t *)buf + u1 * bl;
+        out[n++].iov_len = (b - u1) * bl;
+    }
+    return n;
+}
+
+int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
+                           const struct draid_stripe_req *req, const struct iovec *iov,
+                           int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
+                           int *nreads)
+{
+    if (!r || !ctx || !req || !iov || !chunk_buf || !reads || !nreads)
+        return -EINVAL;
+    const int n = r->num_base_bdevs, m = r->max_degraded, k = n - m;
+    const uint64_t s = req->stripe_index, lba = s << r->strip_size_shift;
+    const int pdisk = req->p_disk, qdisk = req->q_disk;
+    /* R = [lo, hi): the requested ranges of degraded data chunks (raid5.c:882-891
+     * picks the one d_chunk; RAID6 may have two) */
+    uint64_t lo = r->strip_size, hi = 0;
+    int ndeg = 0;
+    for (int disk = 0; disk < n; disk++) {
+        if (!(r->degraded_mask & (1u << disk)))
+            continue;
+        ndeg++;
+        const struct draid_chunk_req *c = &req->chunk[disk];
+        if (disk == pdisk || disk == qdisk || !c->req_blocks)
+            continue;
+        if (c->req_offset < lo)
+            lo = c->req_offset;
+        if (c->req_offset + c->req_blocks > hi)
+            hi = c->req_offset + c->req_blocks;
+    }
+    int nr = 0, rc;
+    if (hi <= lo) { /* nothing to rebuild: plain reads (raid5.c:933-945) */
+        for (int d = req->first_data; d <= req->last_data; d++) {
+            if (!req->chunk[draid_raid_data_disk(r, s, d)].req_blocks)
+                continue;
+            if ((rc = read_request(r, req, d, iov, iovcnt, &reads[nr++])) < 0)
+                return rc;
+        }
+        *nreads = nr;
+        return 0;
+    }
+    if (ndeg > m)
+        return -EIO;
+    /* lost strips in isa-l order; a read never regenerates Q, so a lost Q is
+     * left out and Q is read only when two strips are lost */
+    int fail[2], nfail = 0;
+    for (int disk = 0; disk < n; disk++)
+        if ((r->degraded_mask & (1u << disk)) && disk != qdisk)
+            fail[nfail++] = disk == pdisk ? k : draid_raid_disk_data_index(r, s, disk);
+    const int needq = nfail == 2;
+    static __thread struct iovec lv[DRAID_RAID_MAX_BASE][DRAID_RAID_MAX_IOV + 2];
+    const struct iovec *lists[DRAID_RAID_MAX_BASE];
+    int cnts[DRAID_RAID_MAX_BASE];
+    for (int j = 0; j < n; j++) {
+        const int disk = j < k ? draid_raid_data_disk(r, s, j) : (j == k ? pdisk : qdisk);
+        const int d = j < k ? j : -1;
+        const struct draid_chunk_req *c = &req->chunk[disk];
+        /* sources and rebuilt outputs over R: requested parts in the parent
+         * iovecs, the rest in chunk_buf (a lost Q, or Q when unneeded, is never
+         * touched by the kernel) */
+        const int cnt = range_list(r, req, disk, d, lo, hi, iov, iovcnt, chunk_buf[disk], lv[j],
+                                   DRAID_RAID_MAX_IOV + 2);
+        if (cnt < 0)
+            return cnt;
+        lists[j] = lv[j];
+        cnts[j] = cnt;
+        if ((r->degraded_mask & (1u << disk)) || (disk == qdisk && !needq))
+            continue;
+        if (d >= 0 && c->req_blocks && (rc = read_request(r, req, d, iov, iovcnt, &reads[nr++])) < 0)
+            return rc;
+        /* the parts of R its request does not cover (CHUNK_PREREAD, raid5.c:896-917) */
+        uint64_t u0, u1;
+        covered(c, d, lo, hi, &u0, &u1);
+        if (lo < u0)
+            add_io(&reads[nr++], disk, lba, lo, u0 - lo, chunk_buf[disk], r->blocklen);
+        if (u1 < hi)
+            add_io(&reads[nr++], disk, lba, u1, hi - u1, chunk_buf[disk], r->blocklen);
+    }
+    *nreads = nr;
+    rc = draid_ec_ctx_reconstruct_sg(ctx, (uint32_t)k, (uint32_t)m, lists, cnts, NULL,
+                                     (hi - lo) * r->blocklen, nfail, fail);
+    return rc > 0 ? -EINVAL : rc;
+}

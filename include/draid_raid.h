@@ -141,6 +141,26 @@ int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ct
                                     uint64_t stripe, void *const *chunk_buf,
                                     struct draid_base_io *reads, int *nreads);
 
+/* Ranged read of one stripe request (raid5_stripe_read, raid5.c:869-946, and
+ * raid5_complete_reconstructed_stripe_request, raid5.c:544-594, generalised to
+ * RAID6).  Healthy: one base read per requested data chunk straight into the
+ * parent iovecs.  With requested data chunks on degraded disks, R = the union of
+ * their requested ranges is rebuilt, as the reference rebuilds d_chunk's range:
+ * every other needed strip is read over R (Q only when two strips are lost) and
+ * the reconstruct of R is queued on ctx.  Unlike the reference, which prereads
+ * the union of a requested chunk's range and R into a stripe buffer and then
+ * memcpys the requested part back (raid5.c:910-917,572-590), the parts of R a
+ * request covers are read into the parent iovecs, the rest into chunk_buf, and
+ * the kernel gathers R from both: no copy pass.  Lost requested ranges are
+ * rebuilt straight into the parent iovecs.  chunk_buf[disk] are strip-sized
+ * scratch buffers; reads[] must hold 3 * n entries.  Once the base reads are
+ * in, draid_ec_ctx_flush + query/synchronize finish the request.  -EIO if a
+ * rebuild is needed and more disks are degraded than the level tolerates. */
+int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
+                           const struct draid_stripe_req *req, const struct iovec *iov,
+                           int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
+                           int *nreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -326,6 +326,95 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
     int nr;
     CHECK(draid_raid_stripe_degraded_read(&r, ctx, 0, (void *const *)chunk, rd, &nr) == -EIO);
 
+    /* ranged reads (raid5_stripe_read): the reference's read request grid
+     * (raid5_ut_ref.c:439-463) on the first min(n, stripes) stripes plus random
+     * requests, each healthy, with one and (RAID6) two degraded disks, and with
+     * one more than the level tolerates; the bytes must arrive in the parent
+     * iovecs exactly as the writes above left them. */
+    uint8_t *ubuf, *ujunk, *hr = malloc(ub);
+    HIPOK(draid_ec_device_alloc((void **)&ubuf, ub));
+    HIPOK(draid_ec_device_alloc((void **)&ujunk, ub));
+    memset(hr, 0x5A, ub);
+    HIPOK(draid_ec_memcpy_async(ujunk, hr, ub, 0, st));
+    static struct draid_base_io rio[3 * DRAID_RAID_MAX_BASE];
+    const uint64_t grid[][2] = {{0, 1},          {0, strip},          {0, strip + 1},
+                                {0, r.stripe_blocks}, {1, 1},          {1, strip},
+                                {1, strip + 1},  {strip, 1},          {strip, strip},
+                                {strip, strip + 1}, {strip - 1, 1},   {strip - 1, strip},
+                                {strip - 1, strip + 1}, {strip - 1, 2}};
+    const int ngrid = (int)(sizeof(grid) / sizeof(grid[0]));
+    const uint64_t ns = r.total_stripes < (uint64_t)n ? r.total_stripes : (uint64_t)n;
+    int rebuilt = 0, refused = 0, nreq = 0;
+    for (int t = 0; t < ngrid * (int)ns + 64; t++) {
+        uint64_t s, off, len;
+        if (t < ngrid * (int)ns) {
+            s = (uint64_t)(t % (int)ns);
+            off = grid[t / (int)ns][0];
+            len = grid[t / (int)ns][1];
+            if (off + len > r.stripe_blocks)
+                continue;
+        } else {
+            s = orc_splitmix64(&rng) % r.total_stripes;
+            off = orc_splitmix64(&rng) % r.stripe_blocks;
+            len = 1 + orc_splitmix64(&rng) % (r.stripe_blocks - off);
+        }
+        struct draid_stripe_req q;
+        CHECK(draid_raid_map_request(&r, s * r.stripe_blocks + off, len, &q) == 0);
+        const size_t nb = len * blocklen, h = nb / 3;
+        struct iovec uiov[3] = {{ubuf, h}, {ubuf + h, 0}, {ubuf + h, nb - h}};
+        for (int nd = 0; nd <= m + 1; nd++) {
+            uint32_t mask = 0;
+            while (__builtin_popcount(mask) < nd)
+                mask |= 1u << (orc_splitmix64(&rng) % (uint64_t)n);
+            if (nd == 1) /* always a rebuild */
+                mask = 1u << draid_raid_data_disk(&r, s, q.first_data);
+            r.degraded_mask = mask;
+            int lost_req = 0;
+            for (int disk = 0; disk < n; disk++)
+                if ((mask >> disk & 1u) && disk != q.p_disk && disk != q.q_disk &&
+                    q.chunk[disk].req_blocks)
+                    lost_req = 1;
+            for (int d = 0; d < n; d++)
+                d2d(chunk[d], junk, sb, st);
+            d2d(ubuf, ujunk, nb, st);
+            int nio = -1;
+            const int rc = draid_raid_stripe_read(&r, ctx, &q, uiov, 3, (void *const *)chunk, rio,
+                                                  &nio);
+            nreq++;
+            if (lost_req && nd > m) {
+                CHECK(rc == -EIO);
+                refused++;
+                continue;
+            }
+            CHECK(rc == 0);
+            if (rc)
+                continue;
+            rebuilt += lost_req;
+            CHECK(nio <= 3 * n);
+            for (int i = 0; i < nio; i++) { /* fake base reads */
+                CHECK(!(mask & (1u << rio[i].disk)));
+                size_t o = (size_t)rio[i].offset_blocks * blocklen;
+                for (int v = 0; v < rio[i].iovcnt; v++) {
+                    if (rio[i].iov[v].iov_len)
+                        d2d(rio[i].iov[v].iov_base, disk[rio[i].disk] + o, rio[i].iov[v].iov_len,
+                            st);
+                    o += rio[i].iov[v].iov_len;
+                }
+                CHECK(o == (size_t)(rio[i].offset_blocks + rio[i].num_blocks) * blocklen);
+            }
+            HIPOK(draid_ec_ctx_flush(ctx));
+            HIPOK(draid_ec_ctx_synchronize(ctx));
+            HIPOK(draid_ec_memcpy_async(hr, ubuf, nb, 1, st));
+            HIPOK(draid_ec_ctx_synchronize(ctx));
+            CHECK(cmp_host(hr, hu + s * ub + off * blocklen, nb));
+        }
+    }
+    CHECK(rebuilt > 0 && refused > 0);
+    r.degraded_mask = 0;
+    draid_ec_device_free(ubuf);
+    draid_ec_device_free(ujunk);
+    free(hr);
+
     for (int d = 0; d < n; d++) {
         draid_ec_device_free(disk[d]);
         draid_ec_device_free(chunk[d]);
@@ -340,9 +429,10 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
     free(ref);
     free(hc);
     draid_ec_ctx_destroy(ctx);
-    printf("  raid%d n=%d blocklen=%u strip=%uKiB (partial writes rmw=%d rcw=%d): %s\n", lvl, n,
-           blocklen, strip_kb, modes[DRAID_WRITE_RMW], modes[DRAID_WRITE_RCW],
-           g_fail ? "FAIL" : "ok");
+    printf("  raid%d n=%d blocklen=%u strip=%uKiB (partial writes rmw=%d rcw=%d; ranged reads %d, "
+           "%d rebuilt, %d refused): %s\n",
+           lvl, n, blocklen, strip_kb, modes[DRAID_WRITE_RMW], modes[DRAID_WRITE_RCW], nreq,
+           rebuilt, refused, g_fail ? "FAIL" : "ok");
 }
 
 int main(int argc, char **argv)
