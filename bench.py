@@ -81,12 +81,15 @@ CONFIGS = {
     "raid5_4p1_64k": dict(k=4, m=1, strip_kib=64, stripes=4096, failures="single",
                           label="RAID5 4+1 XOR encode + single-failure reconstruct, 64 KiB "
                                 "strips (configs[1])"),
-    # configs[3] -- RAID6 8+2 single-failure degraded read, 128 KiB
-    "raid6_8p2_128k_single": dict(k=8, m=2, strip_kib=128, stripes=4096, failures="single",
+    # configs[3] -- RAID6 8+2 single-failure degraded read, 128 KiB; strong scaling
+    # (--strong) splits 16384 stripes (20 GiB) over the ranks
+    "raid6_8p2_128k_single": dict(k=8, m=2, strip_kib=128, stripes=4096, strong_stripes=16384,
+                                  failures="single",
                                   label="RAID6 8+2 encode + single-failure reconstruct, 128 KiB "
                                         "strips (configs[3])"),
     # configs[4] -- RAID6 16+2 dual failure, 256 KiB; 4096 stripes over 8 GPUs = 512 per GPU
-    "raid6_16p2_256k_dual": dict(k=16, m=2, strip_kib=256, stripes=512, failures="dual",
+    "raid6_16p2_256k_dual": dict(k=16, m=2, strip_kib=256, stripes=512, strong_stripes=4096,
+                                 failures="dual",
                                  label="RAID6 16+2 encode + dual-data-failure reconstruct, 256 KiB "
                                        "strips (configs[4])"),
 }
@@ -145,7 +148,11 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="raid6_8p2_64k", choices=sorted(CONFIGS))
-    ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (override)")
+    ap.add_argument("--stripes", type=int, default=None,
+                    help="stripes per GPU (override); with --strong, the whole job's")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: a fixed stripe count (the config's strong_stripes) "
+                         "sharded across the ranks instead of a fixed count per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -181,7 +188,12 @@ def main() -> None:
 
     cfg = CONFIGS[args.config]
     k, m, S = cfg["k"], cfg["m"], cfg["strip_kib"] * 1024
-    B = args.stripes or cfg["stripes"]
+    if args.strong:  # fixed total, contiguous stripe ranges per rank
+        total = args.stripes or cfg.get("strong_stripes", cfg["stripes"])
+    else:            # weak scaling: B stripes per GPU
+        total = (args.stripes or cfg["stripes"]) * world
+    lo, hi = shard_range(total, rank, world)  # this rank's global stripe indices
+    B = hi - lo
     n = k + m
     # Stripe-major layout in HBM: stripe s = [D0 .. D{k-1} P Q], strips contiguous.
     buf = torch.empty(B * n * S, dtype=torch.uint8, device=dev)
@@ -191,7 +203,6 @@ def main() -> None:
     view[:, :k] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
     base = buf.data_ptr()
     table = (base + torch.arange(B * n, dtype=torch.int64, device=dev) * S).contiguous()
-    lo, hi = shard_range(B * world, rank, world)  # this rank's global stripe indices
     fgen = failure_pairs if cfg["failures"] == "dual" else failure_single
     fail_np = fgen(B, k, 0x1234 ^ lo)
     fail = torch.from_numpy(fail_np.reshape(-1)).to(dev)
@@ -277,17 +288,20 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (uniform random bytes, torch Generator seed 0x1234+rank)",
         "config": {
-            "workload": f"{cfg['label']}, {B} stripes per GPU",
+            "workload": f"{cfg['label']}, " + (f"{total} stripes over {world} GPU(s)"
+                                                 if args.strong else f"{B} stripes per GPU"),
             "name": workload, "k": k, "m": m, "strip_bytes": S, "stripes_per_gpu": B,
+            "stripes_total": total,
             "failures": cfg["failures"],
             "layout": "stripe-major contiguous, device pointer table",
             "parallelism": f"stripe-sharded x{world}, no collectives",
         },
+        **({"lab_variant": args.variant} if args.variant else {}),
         "breakdown": {
             "encode_ms": round(enc_ms, 4),
             "reconstruct_ms": round(rec_ms, 4),

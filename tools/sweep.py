@@ -29,7 +29,11 @@ VARIANTS = {0: "default (64 lanes U1)", 1: "U2", 2: "512 lanes U1", 3: "128 lane
             13: "DIAG no-plan U2", 14: "DIAG no-plan U1", 15: "DIAG no-plan no-mul U1",
             16: "XCD-aware map", 17: "XCD-aware 512 lanes",
             18: "64 lanes U2", 19: "64 lanes U4", 20: "64 lanes XCD-aware",
-            21: "64 lanes nt loads only", 22: "64 lanes nt stores only",23: "64 lanes no nt"}
+            21: "64 lanes nt loads only", 22: "64 lanes nt stores only", 23: "64 lanes no nt",
+            24: "st buffer nt", 25: "st sc1", 26: "st sc1 nt", 27: "st sc0 sc1 nt",
+            28: "st sc0 nt", 29: "ld buffer nt", 30: "ld sc1 nt", 31: "ld sc0 sc1 nt",
+            32: "ld sc0 nt", 33: "ld sc1 st sc1", 34: "ld buf nt st sc1 nt",
+            35: "ld buf nt st buf nt", 36: "ld buf nt st sc1", 37: "ld sc0sc1nt st sc1nt"}
 
 
 def probe(torch, dev, nbytes, rounds, iters):
@@ -119,6 +123,34 @@ def main():
         buf, table = make_layout(torch, name, k, m, S, B, dev)
         layouts[name] = (buf, table, ec.make_batch(k, m, S, B, table))
     variants = [int(v) for v in args.variants.split(",")]
+    verified = {}
+    if "stripe_major" in layouts:
+        # every variant must produce the default's bytes: erase its outputs, rerun, compare
+        buf, _, batch = layouts["stripe_major"]
+        view = buf.view(B, k + m, S)
+        ec.set_variant(0)
+        ec.encode(batch, sh)
+        torch.cuda.synchronize(dev)
+        good = view.clone()
+        fnp = fgen(B, k, 0x1234)
+        rows = torch.arange(B, device=dev)
+        for v in variants:
+            ec.set_variant(v)
+            view[:, k:] = 0
+            ec.encode(batch, sh)
+            torch.cuda.synchronize(dev)
+            ok = torch.equal(view, good)
+            for slot in range(2):
+                idx = np.nonzero(fnp[:, slot] != 0xFF)[0]
+                if len(idx):
+                    ii = torch.from_numpy(idx).to(dev)
+                    view[rows[ii], torch.from_numpy(fnp[idx, slot].astype(np.int64)).to(dev)] = 0
+            ec.reconstruct(batch, fail, sh)
+            torch.cuda.synchronize(dev)
+            verified[v] = ok and torch.equal(view, good)
+            print(f"verify v{v}: {'ok' if verified[v] else 'MISMATCH'}")
+        del good
+        ec.set_variant(0)
     res = {f"{l}|{v}|{op}": [] for l in layouts for v in variants for op in ("enc", "rec")}
     nbytes = (k + m) * S * B
     rec_nbytes = bench.reconstruct_bytes_per_stripe(k, m, S, args.failures) * B
@@ -145,6 +177,7 @@ def main():
         lname, v, op = key.split("|")
         med = float(np.median(vals))
         summary.append({"layout": lname, "variant": int(v), "desc": VARIANTS[int(v)], "op": op,
+                        "verified": verified.get(int(v)),
                         "median_us": round(med, 2), "min_us": round(min(vals), 2),
                         "hbm_gb_s": round((nbytes if op == "enc" else rec_nbytes) / (med * 1e-6)
                                           / 1e9, 1)})
