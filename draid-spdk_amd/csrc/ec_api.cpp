@@ -381,6 +381,25 @@ int draid_ec_host_unregister(void* ptr)
     return e == hipSuccess ? 0 : fail_hip(e, "hipHostUnregister");
 }
 
+int draid_ec_host_device_pointer(const void* ptr, void** dev_ptr)
+{
+    if (!dev_ptr)
+        return fail_arg("host_device_pointer: dev_ptr is NULL");
+    *dev_ptr = nullptr;
+    hipPointerAttribute_t a{};
+    if (!ptr || hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail_arg("host_device_pointer: not a registered or pinned host address");
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer)
+        return fail_arg("host_device_pointer: not a registered or pinned host address");
+    // devicePointer pairs with hostPointer (the start of the mapping)
+    const uint8_t* hp = a.hostPointer ? static_cast<const uint8_t*>(a.hostPointer)
+                                      : static_cast<const uint8_t*>(ptr);
+    *dev_ptr = static_cast<uint8_t*>(a.devicePointer) + (static_cast<const uint8_t*>(ptr) - hp);
+    return 0;
+}
+
 int draid_ec_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream)
 {
     hipMemcpyKind k;

@@ -34,7 +34,7 @@ EXPORTS = (
     "draid_ec_ctx_flush", "draid_ec_ctx_query", "draid_ec_ctx_synchronize",
     "draid_ec_ctx_queued", "draid_ec_host_encode", "draid_ec_host_reconstruct",
     "draid_ec_encode_strided", "draid_ec_reconstruct_strided",
-    "draid_ec_ctx_update_sg",
+    "draid_ec_ctx_update_sg", "draid_ec_host_device_pointer",
 )
 
 
@@ -103,6 +103,7 @@ def lib() -> C.CDLL:
             getattr(L, f).argtypes = [vp]
         L.draid_ec_device_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
         L.draid_ec_host_register.argtypes = [vp, C.c_size_t]
+        L.draid_ec_host_device_pointer.argtypes = [vp, C.POINTER(vp)]
         L.draid_ec_memcpy_async.argtypes = [vp, vp, C.c_size_t, i32, vp]
         L.draid_ec_set_variant.argtypes = [i32]
         L.draid_ec_ctx_create.argtypes = [C.POINTER(vp)]
@@ -217,6 +218,23 @@ def stream_query(stream: int) -> int:
 
 def stream_synchronize(stream: int) -> None:
     _check(lib().draid_ec_stream_synchronize(stream), "stream_synchronize")
+
+
+# ---- host memory ----
+
+def host_register(ptr: int, nbytes: int) -> None:
+    _check(lib().draid_ec_host_register(ptr, nbytes), "host_register")
+
+
+def host_unregister(ptr: int) -> None:
+    _check(lib().draid_ec_host_unregister(ptr), "host_unregister")
+
+
+def host_device_pointer(ptr: int):
+    """Device address of a registered / pinned host byte, or None."""
+    d = C.c_void_p()
+    rc = _check(lib().draid_ec_host_device_pointer(ptr, C.byref(d)), "host_device_pointer")
+    return None if rc else d.value
 
 
 # ---- host-resident stripes ----

@@ -9,7 +9,8 @@
  *     gf_vect_mul.h), re-implemented as HIP kernels on gfx950.  Same argument
  *     meaning, same array order, same 0 / non-zero return convention.  Every
  *     buffer pointer must be device-accessible (hipMalloc'd HBM, or host memory
- *     registered with draid_ec_host_register()).  Calls are synchronous, like
+ *     registered with draid_ec_host_register(), addressed through
+ *     draid_ec_host_device_pointer()).  Calls are synchronous, like
  *     isa-l's: they run on the calling thread's per-thread stream and return
  *     once the result is in memory.
  *
@@ -227,6 +228,12 @@ int draid_ec_device_free(void *ptr);
  * raid5.c:1340-1342) so kernels and DMA can reach it. */
 int draid_ec_host_register(void *ptr, size_t bytes);
 int draid_ec_host_unregister(void *ptr);
+/* The device address of a host byte inside a registered or pinned range: the
+ * pointer to hand to the section 1 / 2 / 2b calls (a registration may map host
+ * memory at a different device address, hipHostGetDevicePointer).  The section
+ * 2c calls take host addresses and translate themselves.  Returns 0, or 1 with
+ * *dev_ptr = NULL when ptr is not in a mapped host range. */
+int draid_ec_host_device_pointer(const void *ptr, void **dev_ptr);
 /* kind: 0 host->device, 1 device->host, 2 device->device. */
 int draid_ec_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *stream);
 

@@ -71,7 +71,7 @@ def lib() -> C.CDLL:
         L.orc_fill_splitmix.argtypes = [vp, sz, C.c_uint64]
         L.orc_fill_ut_ref_pattern.argtypes = [vp, C.c_uint64, u32]
         L.orc_bdevperf_raid5_fsw.restype = C.c_double
-        L.orc_bdevperf_raid5_fsw.argtypes = [i32, sz, sz, C.c_double, C.POINTER(C.c_uint64),
+        L.orc_bdevperf_raid5_fsw.argtypes = [i32, sz, sz, i32, C.c_double, C.POINTER(C.c_uint64),
                                              C.POINTER(C.c_ubyte)]
         _lib = L
     return _lib
@@ -228,9 +228,10 @@ def bench_encode_reconstruct(buf: np.ndarray, k: int, m: int, length: int, nstri
 
 
 def bdevperf_raid5_fsw(n: int = 5, strip: int = 65536, disk_bytes: int = 256 << 20,
-                       seconds: float = 10.0):
+                       seconds: float = 10.0, qd: int = 32):
     """BASELINE config 1 CPU harness: (MiB/s, ios, verified)."""
     ios = C.c_uint64()
     ok = C.c_ubyte()
-    mibs = lib().orc_bdevperf_raid5_fsw(n, strip, disk_bytes, seconds, C.byref(ios), C.byref(ok))
+    mibs = lib().orc_bdevperf_raid5_fsw(n, strip, disk_bytes, qd, seconds, C.byref(ios),
+                                        C.byref(ok))
     return mibs, ios.value, bool(ok.value)

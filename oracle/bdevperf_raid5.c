@@ -8,6 +8,8 @@
  * SPDK + DPDK + isa-l, none of which can be built here, so this harness performs
  * the same per-request data movement on one core:
  *   - stripe index advances sequentially (bdevperf -w write is sequential);
+ *   - qd task buffers of one I/O each, used round-robin (bdevperf allocates one
+ *     buffer per outstanding task, -q 32);
  *   - parity disk p = (n-1) - s mod n, data index d on disk d<p ? d : d+1
  *     (raid5.c:1006-1007, 172-179);
  *   - each data strip is copied into its RAM disk (malloc bdev memcpy,
@@ -31,17 +33,20 @@ static double now_s(void)
 }
 
 /* Returns MiB/s of user data; *ios_out = completed 256 KiB writes.  disk_bytes
- * is the size of each RAM disk; io_size = k * strip (full-stripe writes). */
-double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, double seconds,
+ * is the size of each RAM disk; io_size = k * strip (full-stripe writes); qd task
+ * buffers. */
+double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, int qd, double seconds,
                               uint64_t *ios_out, uint8_t *verify_ok)
 {
     const int k = n - 1;
     const size_t io = (size_t)k * strip;
     const uint64_t stripes = disk_bytes / strip;
     uint8_t **disk = calloc((size_t)n, sizeof(*disk));
-    uint8_t *user = aligned_alloc(4096, io);
+    if (qd < 1)
+        qd = 1;
+    uint8_t *tasks = aligned_alloc(4096, io * (size_t)qd);
     void **vec = calloc((size_t)n, sizeof(*vec));
-    if (!disk || !user || !vec || stripes == 0)
+    if (!disk || !tasks || !vec || stripes == 0)
         return -1.0;
     for (int d = 0; d < n; d++) {
         disk[d] = aligned_alloc(4096, disk_bytes);
@@ -49,7 +54,7 @@ double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, double sec
             return -1.0;
         memset(disk[d], 0, disk_bytes);
     }
-    orc_fill_splitmix(user, io, 0x1234);
+    orc_fill_splitmix(tasks, io * (size_t)qd, 0x1234);
 
     /* isa-l picks its AVX-512 xor_gen on this class of CPU: so does the harness */
     int (*xor_gen)(int, int, void **) = orc_simd_available() ? orc_simd_xor_gen : orc_xor_gen;
@@ -58,6 +63,7 @@ double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, double sec
     do {
         for (int batch = 0; batch < 32; batch++) { /* -q 32 worth per clock check */
             const uint64_t si = s % stripes;
+            uint8_t *user = tasks + (size_t)(s % (uint64_t)qd) * io;
             const int p = (n - 1) - (int)(s % (uint64_t)n);
             for (int d = 0; d < k; d++) {
                 uint8_t *dst = disk[d < p ? d : d + 1] + si * strip;
@@ -90,7 +96,7 @@ double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, double sec
     for (int d = 0; d < n; d++)
         free(disk[d]);
     free(disk);
-    free(user);
+    free(tasks);
     free(vec);
     if (ios_out)
         *ios_out = ios;

@@ -84,7 +84,7 @@ double orc_bench_encode_reconstruct(int k, int m, size_t len, uint32_t nstripes,
                                     double min_seconds, uint64_t *passes);
 
 /* ---- BASELINE config 1 CPU harness (bdevperf_raid5.c) ---- */
-double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, double seconds,
+double orc_bdevperf_raid5_fsw(int n, size_t strip, size_t disk_bytes, int qd, double seconds,
                               uint64_t *ios_out, uint8_t *verify_ok);
 
 /* ---- reference RAID5 geometry (module/bdev/raid/raid5.c) ---- */

@@ -102,3 +102,42 @@ def test_strided_device(ec, k, m, L, B, layout):
     assert ec.reconstruct_strided(d, k, m, L, B, st, ss, fd, stream) == 0
     torch.cuda.synchronize()
     assert (_strips(d.cpu().numpy(), k, m, L, B, st, ss) == ref).all()
+
+
+def test_registered_host_memory(ec):
+    """SPDK's buffers are plain host memory registered once (draid_ec_host_register,
+    raid5.c:1340-1342 hugepages); kernels reach them through the device address
+    draid_ec_host_device_pointer returns, which may differ from the host one."""
+    import ctypes
+    import mmap
+    k, m, L = 6, 2, 8192
+    n = k + m
+    mm = mmap.mmap(-1, n * L + 4096)           # page-aligned anonymous memory
+    buf = np.frombuffer(mm, dtype=np.uint8)
+    base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+    assert ec.host_device_pointer(base) is None  # not registered yet
+    rng = np.random.default_rng(5)
+    buf[:k * L] = rng.integers(0, 256, k * L, dtype=np.uint8)
+    ec.host_register(base, n * L + 4096)
+    try:
+        dev = ec.host_device_pointer(base)
+        assert dev is not None
+        assert ec.host_device_pointer(base + 3 * L + 17) == dev + 3 * L + 17  # interior bytes
+        ref = buf[:n * L].copy().reshape(n, L)
+        assert oracle.encode_strided(ref.reshape(-1), k, m, L, 1, L, n * L) == 0
+        # isa-l-shaped synchronous call over the registered strips
+        assert ec.pq_gen([dev + j * L for j in range(n)], L) == 0
+        assert (buf[:n * L].reshape(n, L) == ref).all()
+        # scatter-gather context over the same memory: rebuild two lost strips
+        buf[1 * L:2 * L] = 0
+        buf[k * L:(k + 1) * L] = 0
+        ctx = ec.Ctx()
+        ctx.reconstruct_sg(k, m, [[(dev + j * L, L)] for j in range(n)], L, [1, k])
+        ctx.flush()
+        ctx.synchronize()
+        ctx.close()
+        assert (buf[:n * L].reshape(n, L) == ref).all()
+    finally:
+        ec.host_unregister(base)
+    del buf
+    mm.close()

@@ -24,9 +24,12 @@ def cpu_model():
 
 def main():
     secs = float(os.environ.get("SECONDS_RUN", "10"))
-    mibs, ios, ok = oracle.bdevperf_raid5_fsw(n=5, strip=65536, disk_bytes=1 << 30, seconds=secs)
+    qd = int(os.environ.get("QD", "32"))
+    mibs, ios, ok = oracle.bdevperf_raid5_fsw(n=5, strip=65536, disk_bytes=1 << 30, seconds=secs,
+                                              qd=qd)
     r = {"config": "RAID5 4+1 full-stripe write, 64 KiB strip, bdevperf-style over 5 RAM disks",
-         "io_size": 262144, "cores": 1, "seconds": secs, "ios": ios, "mib_s": round(mibs, 1),
+         "io_size": 262144, "qd": qd, "cores": 1, "seconds": secs, "ios": ios,
+         "mib_s": round(mibs, 1),
          "iops": round(ios / secs, 1), "parity_verified": ok, "cpu": cpu_model(),
          "xor_gen": "AVX-512 restatement of isa-l xor_gen_avx512 (oracle/isal_simd.c)"
          if oracle.simd_available() else "scalar restatement",
