@@ -161,6 +161,46 @@ int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
                            int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
                            int *nreads);
 
+/* ------------------------------------------------------------------------
+ * Stripe cache and per-stripe request queue (raid5_get_stripe /
+ * raid5_reclaim_stripes, raid5.c:1057-1131; the stripe's request list,
+ * raid5.c:1047-1054,485-521).  A fixed pool of nslots entries (RAID_MAX_STRIPES,
+ * bdev_raid.h:39, in the reference); entry i owns slot i of a stripe region the
+ * caller allocates -- n strips of strip bytes per slot, stripe-major, in HBM or
+ * registered host memory -- so a batch of cached stripes is one
+ * draid_ec_strided_stripes descriptor.  Thread-safe.
+ * ---------------------------------------------------------------------- */
+
+typedef struct draid_stripe_cache draid_stripe_cache;
+
+struct draid_stripe {              /* the public part of a cache entry */
+    uint64_t index;                /* stripe index */
+    uint32_t slot;                 /* its buffers: slot * n * strip bytes into the region */
+};
+
+struct draid_stripe_waiter {       /* one request on a stripe (embedded by the caller) */
+    struct draid_stripe_waiter *next;
+    void *arg;
+};
+
+int draid_stripe_cache_create(draid_stripe_cache **cache, uint32_t nslots);
+void draid_stripe_cache_destroy(draid_stripe_cache *cache);
+/* Looks the stripe up or claims an entry for it (reclaiming unreferenced
+ * least-recently-used entries when none is free) and takes a reference.  NULL
+ * when every entry is referenced: queue the request and retry after a put
+ * (raid5.c:1310-1318). */
+struct draid_stripe *draid_stripe_get(draid_stripe_cache *cache, uint64_t index);
+void draid_stripe_put(draid_stripe_cache *cache, struct draid_stripe *stripe);
+/* Appends a request to the stripe's queue: 1 = it is the only one, submit it
+ * now; 0 = it waits for the requests ahead of it. */
+int draid_stripe_enqueue(draid_stripe_cache *cache, struct draid_stripe *stripe,
+                         struct draid_stripe_waiter *w);
+/* Removes a finished request; returns the next request to submit, or NULL. */
+struct draid_stripe_waiter *draid_stripe_complete(draid_stripe_cache *cache,
+                                                  struct draid_stripe *stripe,
+                                                  struct draid_stripe_waiter *w);
+uint32_t draid_stripe_cache_active(draid_stripe_cache *cache); /* entries mapped to stripes */
+
 #ifdef __cplusplus
 }
 #endif

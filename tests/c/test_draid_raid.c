@@ -9,6 +9,7 @@
  * `--cpu-only` runs only the host logic (geometry, request and iovec mapping).
  */
 #include <errno.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -145,6 +146,128 @@ static void test_mapping(void)
     CHECK(draid_raid_map_iov(out, 4, par, 3, 95, 10) == -EINVAL);
     CHECK(draid_raid_map_iov(out, 1, par, 3, 0, 20) == -ENOSPC);
     CHECK(draid_raid_map_iov(out, 4, par, 3, 0, 10) == 1);
+}
+
+/* Stripe cache and request queue (raid5.c:1047-1131, 485-521). */
+static void test_stripe_cache(void)
+{
+    draid_stripe_cache *c;
+    CHECK(draid_stripe_cache_create(&c, 0) == -EINVAL);
+    CHECK(draid_stripe_cache_create(&c, 16) == 0);
+    struct draid_stripe *a = draid_stripe_get(c, 7), *b = draid_stripe_get(c, 7);
+    CHECK(a && a == b && a->index == 7 && a->slot < 16); /* one entry per stripe, two refs */
+    CHECK(draid_stripe_cache_active(c) == 1);
+    /* request queue: first runs at once, the others wait in arrival order */
+    struct draid_stripe_waiter w[3];
+    CHECK(draid_stripe_enqueue(c, a, &w[0]) == 1);
+    CHECK(draid_stripe_enqueue(c, a, &w[1]) == 0);
+    CHECK(draid_stripe_enqueue(c, a, &w[2]) == 0);
+    CHECK(draid_stripe_complete(c, a, &w[0]) == &w[1]);
+    CHECK(draid_stripe_complete(c, a, &w[2]) == NULL); /* a non-head leaves quietly */
+    CHECK(draid_stripe_complete(c, a, &w[1]) == NULL);
+    CHECK(draid_stripe_enqueue(c, a, &w[0]) == 1);
+    CHECK(draid_stripe_complete(c, a, &w[0]) == NULL);
+    draid_stripe_put(c, a);
+    draid_stripe_put(c, b);
+    /* fill every slot with referenced stripes: the next miss has nothing to reclaim */
+    struct draid_stripe *held[16];
+    int slots_seen[16] = {0};
+    for (int i = 0; i < 16; i++) {
+        held[i] = draid_stripe_get(c, 100 + (uint64_t)i);
+        CHECK(held[i] != NULL);
+        if (held[i])
+            slots_seen[held[i]->slot]++;
+    }
+    for (int i = 0; i < 16; i++)
+        CHECK(slots_seen[i] == 1);
+    CHECK(draid_stripe_get(c, 999) == NULL);
+    /* release the four least recently used: a miss reclaims from the LRU end */
+    for (int i = 0; i < 4; i++)
+        draid_stripe_put(c, held[i]);
+    struct draid_stripe *n1 = draid_stripe_get(c, 999);
+    CHECK(n1 != NULL && n1->index == 999);
+    CHECK(draid_stripe_cache_active(c) <= 16);
+    for (int i = 4; i < 16; i++) /* still-referenced entries were never reclaimed */
+        CHECK(draid_stripe_get(c, 100 + (uint64_t)i) == held[i]);
+    draid_stripe_cache_destroy(c);
+}
+
+/* Many threads issuing requests on a few hot stripes: per stripe at most one
+ * request runs at a time, none is lost, and every entry is released. */
+enum { ST_THREADS = 8, ST_REQS = 20000, ST_STRIPES = 12, ST_SLOTS = 8 };
+struct st_req {
+    struct draid_stripe_waiter w;
+    struct draid_stripe *s;
+    int done;
+};
+static draid_stripe_cache *g_sc;
+static int g_running[ST_STRIPES];
+static long g_completed;
+static int g_violations;
+
+static void st_run(struct st_req *r) /* the "stripe request" body */
+{
+    const uint64_t idx = r->s->index;
+    if (__atomic_add_fetch(&g_running[idx], 1, __ATOMIC_SEQ_CST) != 1)
+        __atomic_add_fetch(&g_violations, 1, __ATOMIC_SEQ_CST);
+    for (volatile int spin = 0; spin < 200; spin++) /* hold the stripe a little while */
+        ;
+    __atomic_sub_fetch(&g_running[idx], 1, __ATOMIC_SEQ_CST);
+}
+
+static void *st_thread(void *arg)
+{
+    uint64_t rng = 0x1234 + (uint64_t)(uintptr_t)arg;
+    static __thread struct st_req reqs[64];
+    for (int i = 0; i < ST_REQS; i++) {
+        struct st_req *r = &reqs[i % 64];
+        /* its previous request may still wait in a stripe queue: the thread walking
+         * that queue runs it (nothing blocks), then the slot is free again */
+        while (i >= 64 && !__atomic_load_n(&r->done, __ATOMIC_ACQUIRE))
+            ;
+        r->done = 0;
+        const uint64_t idx = orc_splitmix64(&rng) % ST_STRIPES;
+        struct draid_stripe *s;
+        while (!(s = draid_stripe_get(g_sc, idx))) /* every entry referenced: retry */
+            ;
+        r->s = s;
+        r->w.arg = r;
+        if (draid_stripe_enqueue(g_sc, s, &r->w) != 1)
+            continue; /* queued behind a running request; its runner will run this one */
+        /* run the head, then every request it hands on to (this thread's or others') */
+        for (struct draid_stripe_waiter *w = &r->w; w;) {
+            struct st_req *x = w->arg;
+            st_run(x);
+            struct draid_stripe_waiter *next = draid_stripe_complete(g_sc, x->s, w);
+            draid_stripe_put(g_sc, x->s);
+            __atomic_add_fetch(&g_completed, 1, __ATOMIC_SEQ_CST);
+            __atomic_store_n(&x->done, 1, __ATOMIC_RELEASE);
+            w = next;
+        }
+    }
+    for (int i = 0; i < 64; i++) /* drain before the thread-local requests go away */
+        while (!__atomic_load_n(&reqs[i].done, __ATOMIC_ACQUIRE))
+            ;
+    return NULL;
+}
+
+static void test_stripe_cache_threads(void)
+{
+    CHECK(draid_stripe_cache_create(&g_sc, ST_SLOTS) == 0);
+    pthread_t t[ST_THREADS];
+    for (int i = 0; i < ST_THREADS; i++)
+        pthread_create(&t[i], NULL, st_thread, (void *)(uintptr_t)i);
+    for (int i = 0; i < ST_THREADS; i++)
+        pthread_join(t[i], NULL);
+    CHECK(g_completed == (long)ST_THREADS * ST_REQS);
+    CHECK(g_violations == 0);
+    /* every reference released: all stripes reclaimable, so fresh ones fit */
+    for (uint64_t i = 0; i < 3 * ST_SLOTS; i++) {
+        struct draid_stripe *s = draid_stripe_get(g_sc, 1000 + i);
+        CHECK(s != NULL);
+        draid_stripe_put(g_sc, s);
+    }
+    draid_stripe_cache_destroy(g_sc);
 }
 
 /* ---------------------------------------------------------------- GPU tests */
@@ -440,6 +563,8 @@ int main(int argc, char **argv)
     const int cpu_only = argc > 1 && strcmp(argv[1], "--cpu-only") == 0;
     test_geometry();
     test_mapping();
+    test_stripe_cache();
+    test_stripe_cache_threads();
     printf("host logic: %s\n", g_fail ? "FAIL" : "ok");
     if (!cpu_only) {
         const int cfg[][4] = {{5, 3, 512, 4},  {5, 4, 4096, 4},  {5, 5, 512, 64}, {5, 5, 4096, 64},
