@@ -9,13 +9,14 @@
 //   raid5_complete_reconstructed_stripe_request  raid5.c:544-594
 //   D+P / D+D recovery                            gf_vect_mul.c:242-347
 //
-// Shape: one workgroup (256 lanes = 4 waves) owns one chunk of one stripe:
-// CB = 256 * U * 16 bytes of every strip.  Each lane holds U 16-byte vectors
-// per strip; with k known at compile time every source load of the lane is
-// issued before the first XOR, so a wave keeps (k+1)*U KiB in flight.  HBM is
-// the roofline: encode moves (k+m)*S algorithmic bytes per stripe and does
-// ~2 VALU ops per byte read, far below the VALU ceiling.  Workgroups are
-// independent (no inter-workgroup communication, no atomics on the hot path).
+// Shape: one workgroup (one 64-lane wave in production, kLanes below) owns one
+// chunk of one stripe: CB = lanes * U * 16 bytes of every strip (1 KiB).  Each
+// lane holds U 16-byte vectors per strip; with k known at compile time every
+// source load of the lane is issued before the first XOR, so a wave keeps k*U
+// KiB in flight.  HBM is the roofline: encode moves (k+m)*S algorithmic bytes per
+// stripe and does ~2 VALU ops per byte read, far below the VALU ceiling.
+// Workgroups are independent (no inter-workgroup communication, no atomics on
+// the hot path).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
