@@ -583,3 +583,66 @@ int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
                                      (hi - lo) * r->blocklen, nfail, fail);
     return rc > 0 ? -EINVAL : rc;
 }
+
+/* ------------------------------------------------------------ stripe assembly */
+
+void draid_raid_asm_init(struct draid_stripe_asm *a)
+{
+    if (a) {
+        a->active = 0;
+        a->received = 0;
+        a->have = 0;
+    }
+}
+
+/* raid5_submit_write_request, raid5_simple.c:347-423 */
+int draid_raid_asm_add(const struct draid_raid *r, struct draid_stripe_asm *a,
+                       uint64_t offset_blocks, uint64_t num_blocks, const struct iovec *iov,
+                       int iovcnt)
+{
+    if (!r || !a || !iov || iovcnt < 1 || iovcnt > DRAID_RAID_MAX_IOV)
+        return -EINVAL;
+    const uint64_t stripe = offset_blocks / r->stripe_blocks;
+    const uint64_t off = offset_blocks - stripe * r->stripe_blocks;
+    if (num_blocks != r->strip_size || (off & (r->strip_size - 1)) || stripe >= r->total_stripes)
+        return -EINVAL; /* only whole strips of a full-stripe write */
+    const int d = (int)(off >> r->strip_size_shift);
+    uint64_t bytes = 0;
+    for (int i = 0; i < iovcnt; i++)
+        bytes += iov[i].iov_len;
+    if (bytes != (uint64_t)r->strip_size * r->blocklen)
+        return -EINVAL;
+    if (!a->active) { /* the first child of a stripe (raid5_simple.c:356-374) */
+        a->active = 1;
+        a->stripe_index = stripe;
+        a->received = 0;
+        a->have = 0;
+    } else if (a->stripe_index != stripe || (a->have & (1u << d))) {
+        return -EINVAL;
+    }
+    memcpy(a->iov[d], iov, (size_t)iovcnt * sizeof(*iov));
+    a->iovcnt[d] = iovcnt;
+    a->have |= 1u << d;
+    if (++a->received < r->num_base_bdevs - r->max_degraded)
+        return 0;
+    a->active = 0; /* all k data chunks: encode (raid5_simple.c:416-420) */
+    return 1;
+}
+
+int draid_raid_asm_iov(const struct draid_raid *r, const struct draid_stripe_asm *a,
+                       struct iovec *out, int out_max)
+{
+    if (!r || !a || !out)
+        return -EINVAL;
+    const int k = r->num_base_bdevs - r->max_degraded;
+    int n = 0;
+    for (int d = 0; d < k; d++) {
+        if (!(a->have & (1u << d)))
+            return -EINVAL;
+        if (n + a->iovcnt[d] > out_max)
+            return -ENOSPC;
+        memcpy(out + n, a->iov[d], (size_t)a->iovcnt[d] * sizeof(*out));
+        n += a->iovcnt[d];
+    }
+    return n;
+}

@@ -161,6 +161,36 @@ int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
                            int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
                            int *nreads);
 
+/* Stripe assembly of raid5_simple (raid5_submit_write_request,
+ * raid5_simple.c:347-423): with the bdev layer splitting writes at strip
+ * boundaries, a full-stripe write arrives as k strip-sized child I/Os on a
+ * channel; they are gathered per channel (r5ch->current_stripe_request) and the
+ * stripe is encoded once the k-th has arrived.  Children may arrive in any order;
+ * one stripe is assembled at a time. */
+struct draid_stripe_asm {
+    uint64_t stripe_index;
+    int active;                          /* a stripe is being assembled */
+    int received;                        /* data chunks present */
+    uint32_t have;                       /* bit d: data chunk d present */
+    int iovcnt[DRAID_RAID_MAX_BASE];
+    struct iovec iov[DRAID_RAID_MAX_BASE][DRAID_RAID_MAX_IOV];
+};
+
+void draid_raid_asm_init(struct draid_stripe_asm *a);
+/* Adds one child write [offset_blocks, +num_blocks).  Returns 1 when the stripe's
+ * k data chunks are all present (fetch the stripe's parent iovecs with
+ * draid_raid_asm_iov, then draid_raid_stripe_write; the assembler is free
+ * again), 0 while chunks are missing, -EINVAL for a child that is not exactly
+ * one strip (raid5_simple rejects non-full-stripe writes, raid5_simple.c:381-395),
+ * repeats a chunk or belongs to another stripe than the one being assembled. */
+int draid_raid_asm_add(const struct draid_raid *r, struct draid_stripe_asm *a,
+                       uint64_t offset_blocks, uint64_t num_blocks, const struct iovec *iov,
+                       int iovcnt);
+/* The assembled stripe's iovecs in data order (one parent list for the whole
+ * stripe), into out[0 .. out_max); returns the count or -ENOSPC. */
+int draid_raid_asm_iov(const struct draid_raid *r, const struct draid_stripe_asm *a,
+                       struct iovec *out, int out_max);
+
 /* ------------------------------------------------------------------------
  * Stripe cache and per-stripe request queue (raid5_get_stripe /
  * raid5_reclaim_stripes, raid5.c:1057-1131; the stripe's request list,

@@ -148,6 +148,45 @@ static void test_mapping(void)
     CHECK(draid_raid_map_iov(out, 4, par, 3, 0, 10) == 1);
 }
 
+/* raid5_simple stripe assembly (raid5_simple.c:347-423): k strip-sized children in
+ * any order -> one parent list in data order; non-strip, repeated and foreign
+ * children rejected. */
+static void test_stripe_asm(void)
+{
+    struct draid_raid r;
+    CHECK(draid_raid_start(&r, 6, 6, 512, 8, 64 * 8) == 0); /* k = 4, 4 KiB strips */
+    const int k = 4;
+    const size_t sb = 8 * 512;
+    static uint8_t buf[4 * 4096];
+    struct draid_stripe_asm a;
+    draid_raid_asm_init(&a);
+    const uint64_t s = 5, base = s * r.stripe_blocks;
+    const int order[4] = {2, 0, 3, 1};
+    for (int t = 0; t < k; t++) {
+        const int d = order[t];
+        struct iovec ch[2] = {{buf + d * sb, 1000}, {buf + d * sb + 1000, sb - 1000}};
+        if (t == 1) {
+            CHECK(draid_raid_asm_add(&r, &a, base + 8 * 2, 8, ch, 2) == -EINVAL); /* repeat */
+            CHECK(draid_raid_asm_add(&r, &a, base + r.stripe_blocks + 8, 8, ch, 2) == -EINVAL);
+            CHECK(draid_raid_asm_add(&r, &a, base + 8 * d + 1, 7, ch, 2) == -EINVAL); /* partial */
+        }
+        CHECK(draid_raid_asm_add(&r, &a, base + 8 * (uint64_t)d, 8, ch, 2) == (t == k - 1));
+    }
+    struct iovec out[16];
+    const int n = draid_raid_asm_iov(&r, &a, out, 16);
+    CHECK(n == 2 * k);
+    size_t off = 0;
+    for (int i = 0; i < n; i++) { /* data order: one contiguous parent image */
+        CHECK(out[i].iov_base == buf + off);
+        off += out[i].iov_len;
+    }
+    CHECK(off == k * sb);
+    CHECK(draid_raid_asm_iov(&r, &a, out, 3) == -ENOSPC);
+    /* the assembler is free again: a new stripe starts */
+    struct iovec one = {buf, sb};
+    CHECK(draid_raid_asm_add(&r, &a, (s + 1) * r.stripe_blocks, 8, &one, 1) == 0);
+}
+
 /* Stripe cache and request queue (raid5.c:1047-1131, 485-521). */
 static void test_stripe_cache(void)
 {
@@ -323,7 +362,21 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
         struct draid_base_io w[DRAID_RAID_MAX_BASE];
         int nw = 0;
         void *pq[2] = {pbuf[0], pbuf[1]};
-        CHECK(draid_raid_stripe_write(&r, ctx, &q, iov, 3, pq, w, &nw) == 0);
+        if (s & 1) { /* raid5_simple shape: k strip-sized children, last data chunk first */
+            static struct draid_stripe_asm sa;
+            draid_raid_asm_init(&sa);
+            for (int d = k - 1; d >= 0; d--) {
+                struct iovec ch[2] = {{u + d * sb, sb / 2}, {u + d * sb + sb / 2, sb - sb / 2}};
+                CHECK(draid_raid_asm_add(&r, &sa, s * r.stripe_blocks + (uint64_t)d * strip, strip,
+                                         ch, 2) == (d == 0));
+            }
+            struct iovec full[2 * DRAID_RAID_MAX_BASE];
+            const int nf = draid_raid_asm_iov(&r, &sa, full, 2 * DRAID_RAID_MAX_BASE);
+            CHECK(nf == 2 * k);
+            CHECK(draid_raid_stripe_write(&r, ctx, &q, full, nf, pq, w, &nw) == 0);
+        } else {
+            CHECK(draid_raid_stripe_write(&r, ctx, &q, iov, 3, pq, w, &nw) == 0);
+        }
         CHECK(nw == n);
         HIPOK(draid_ec_ctx_flush(ctx));
         /* fake base bdevs: memcpy every base write (raid5_ut_ref.c:284-323) */
@@ -563,6 +616,7 @@ int main(int argc, char **argv)
     const int cpu_only = argc > 1 && strcmp(argv[1], "--cpu-only") == 0;
     test_geometry();
     test_mapping();
+    test_stripe_asm();
     test_stripe_cache();
     test_stripe_cache_threads();
     printf("host logic: %s\n", g_fail ? "FAIL" : "ok");
