@@ -156,6 +156,8 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--layout", default="stripe_major", choices=["stripe_major", "strip_major"],
+                    help="placement of the stripes in HBM (DESIGN.md §3)")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="backend of the timing collectives (nccl = RCCL; gloo only for "
@@ -195,14 +197,22 @@ def main() -> None:
     lo, hi = shard_range(total, rank, world)  # this rank's global stripe indices
     B = hi - lo
     n = k + m
-    # Stripe-major layout in HBM: stripe s = [D0 .. D{k-1} P Q], strips contiguous.
+    # Stripes in HBM.  stripe_major: stripe s = [D0 .. D{k-1} P Q], strips contiguous
+    # (one stripe-cache slot per stripe); strip_major: one region per strip index j
+    # holding strip j of every stripe.  The kernels only see the pointer table.
     buf = torch.empty(B * n * S, dtype=torch.uint8, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(0x1234 + rank)
-    view = buf.view(B, n, S)
-    view[:, :k] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
     base = buf.data_ptr()
-    table = (base + torch.arange(B * n, dtype=torch.int64, device=dev) * S).contiguous()
+    if args.layout == "stripe_major":
+        view = buf.view(B, n, S)
+        table = (base + torch.arange(B * n, dtype=torch.int64, device=dev) * S).contiguous()
+    else:
+        view = buf.view(n, B, S).permute(1, 0, 2)  # [stripe, strip, byte] over the regions
+        si = torch.arange(B, dtype=torch.int64, device=dev).repeat_interleave(n)
+        sj = torch.arange(n, dtype=torch.int64, device=dev).repeat(B)
+        table = (base + (sj * B + si) * S).contiguous()
+    view[:, :k] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
     fgen = failure_pairs if cfg["failures"] == "dual" else failure_single
     fail_np = fgen(B, k, 0x1234 ^ lo)
     fail = torch.from_numpy(fail_np.reshape(-1)).to(dev)
@@ -298,7 +308,8 @@ def main() -> None:
             "name": workload, "k": k, "m": m, "strip_bytes": S, "stripes_per_gpu": B,
             "stripes_total": total,
             "failures": cfg["failures"],
-            "layout": "stripe-major contiguous, device pointer table",
+            "layout": ("stripe-major contiguous" if args.layout == "stripe_major" else
+                       "strip-major (one region per strip index)") + ", device pointer table",
             "parallelism": f"stripe-sharded x{world}, no collectives",
         },
         **({"lab_variant": args.variant} if args.variant else {}),
