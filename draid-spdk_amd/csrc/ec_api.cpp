@@ -243,6 +243,9 @@ static int check_batch(const draid_ec_stripe_batch* b)
         return fail_arg("batch needs 1 <= k <= 255, m in {1,2}, flags == 0");
     if (b->nstripes && (!b->strips || b->strip_len == 0))
         return b->strip_len == 0 ? 0 : fail_arg("batch strips table is NULL");
+    if (!draid::launch_fits(b->strip_len, b->nstripes))
+        return fail_arg("batch too large for one launch (strip_len <= 0x7fff0000, "
+                        "ceil(strip_len / 1 KiB) * nstripes < 2^31)");
     return 0;
 }
 
@@ -278,6 +281,9 @@ static int check_strided(const draid_ec_strided_stripes* d)
         return fail_arg("strided stripes need 1 <= k <= 255, m in {1,2}, flags == 0");
     if (d->nstripes && d->strip_len && !d->base)
         return fail_arg("strided stripes base is NULL");
+    if (!draid::launch_fits(d->strip_len, d->nstripes))
+        return fail_arg("stripes too large for one launch (strip_len <= 0x7fff0000, "
+                        "ceil(strip_len / 1 KiB) * nstripes < 2^31)");
     return 0;
 }
 

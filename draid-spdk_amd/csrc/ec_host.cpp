@@ -127,6 +127,9 @@ int check_host(const draid_ec_host_stripes* h)
                                "DRAID_EC_HOST_STAGED}");
     if (h->strip_stride < h->strip_len)
         return draid::fail_arg("strip_stride < strip_len");
+    if (!draid::launch_fits(h->strip_len, h->nstripes))
+        return draid::fail_arg("stripes too large for one launch (strip_len <= 0x7fff0000, "
+                               "ceil(strip_len / 1 KiB) * nstripes < 2^31)");
     return 0;
 }
 

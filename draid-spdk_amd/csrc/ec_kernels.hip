@@ -26,8 +26,6 @@
 namespace draid {
 
 constexpr int kThreads = 256;
-// Largest strip a launch accepts: in-kernel offsets are 32-bit.
-constexpr uint64_t kMaxStripLen = 0x7fff0000ull;
 
 __constant__ GfTables c_gf = make_gf_tables();
 

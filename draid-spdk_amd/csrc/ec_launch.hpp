@@ -11,6 +11,17 @@ namespace draid {
 // arguments (one stripe); above this many vectors they go through a device table.
 constexpr int kMaxArgPtrs = 34;
 
+// Launch limits (argument errors, checked before any launch): in-kernel strip
+// offsets are 32-bit, and one launch covers at most 2^31 - 1 work items of
+// kItemBytes of every strip of a stripe.
+constexpr uint64_t kMaxStripLen = 0x7fff0000ull;
+constexpr uint64_t kItemBytes = 1024;
+inline bool launch_fits(uint64_t strip_len, uint64_t nstripes)
+{
+    return strip_len <= kMaxStripLen &&
+           (strip_len + kItemBytes - 1) / kItemBytes * nstripes <= 0x7fffffffull;
+}
+
 struct ArgPtrTable {
     const uint8_t* p[kMaxArgPtrs];
 };

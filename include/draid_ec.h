@@ -102,7 +102,9 @@ typedef struct draid_ec_stripe_batch {
 } draid_ec_stripe_batch;
 
 /* Full-stripe encode of every stripe in the batch (P for m == 1, P and Q for
- * m == 2).  Enqueued on `stream`; returns without waiting. */
+ * m == 2).  Enqueued on `stream`; returns without waiting.  One call covers
+ * strip_len <= 0x7fff0000 and ceil(strip_len / 1 KiB) * nstripes < 2^31 (else 1,
+ * as for every batched / strided / host call). */
 int draid_ec_encode(const draid_ec_stripe_batch *batch, void *stream);
 
 /* Degraded-read / rebuild reconstruct.  `fail` is a DEVICE array of

@@ -65,3 +65,31 @@ def test_abi_version_and_host_gf():
             assert draid_ec.gf_mul(a, b) == oracle.gf_mul(a, b)
     for c in (0, 1, 2, 0x1D, 0x8E, 0xFF):
         assert draid_ec.gf_vect_mul_init(c) == bytes(oracle.gf_vect_mul_init(c))
+
+
+def test_argument_errors_before_any_launch():
+    """Rejected arguments return 1 (isa-l style) before any HIP call, so this runs
+    without a GPU: bad k/m/flags, NULL tables, and launches too large for one grid."""
+    import ctypes as C
+    L = draid_ec.lib()
+    dummy = C.c_void_p(0x1000)
+    cases = [
+        draid_ec.StripeBatch(0, 2, 4096, 1, 0, dummy.value),        # k = 0
+        draid_ec.StripeBatch(8, 3, 4096, 1, 0, dummy.value),        # m = 3
+        draid_ec.StripeBatch(8, 2, 4096, 1, 7, dummy.value),        # flags != 0
+        draid_ec.StripeBatch(8, 2, 4096, 1, 0, None),               # no table
+        draid_ec.StripeBatch(8, 2, 0x80000000, 1, 0, dummy.value),  # strip > 0x7fff0000
+        draid_ec.StripeBatch(8, 2, 1 << 30, 4096, 0, dummy.value),  # 2^32 work items
+    ]
+    for b in cases:
+        assert L.draid_ec_encode(C.byref(b), None) == 1, draid_ec.last_error()
+    assert L.draid_ec_reconstruct(C.byref(cases[-1]), dummy, None) == 1
+    assert "too large" in draid_ec.last_error()
+    h = draid_ec.HostStripes(8, 2, 1 << 30, 4096, 0, dummy.value, 1 << 30, 10 << 30)
+    assert L.draid_ec_encode_strided(C.byref(h), None) == 1
+    assert L.draid_ec_host_encode(C.byref(h), 0) == 1
+    # isa-l contracts of the synchronous calls
+    arr = (C.c_void_p * 4)(*([dummy.value] * 4))
+    assert L.draid_xor_gen(2, 64, arr) == 1           # fewer than 2 sources + dest
+    assert L.draid_pq_gen(4, 48, arr) == 1            # len % 32 != 0
+    assert L.draid_gf_vect_mul(31, bytes(32), dummy, dummy) == 1
