@@ -646,3 +646,53 @@ int draid_raid_asm_iov(const struct draid_raid *r, const struct draid_stripe_asm
     }
     return n;
 }
+
+/* ------------------------------------------------------------ disk-level tables */
+
+int draid_raid_fail_table(const struct draid_raid *r, uint64_t first, uint32_t count,
+                          uint8_t *fail)
+{
+    if (!r || !fail)
+        return -EINVAL;
+    const int n = r->num_base_bdevs, m = r->max_degraded, k = n - m;
+    int deg[2], nd = 0;
+    for (int disk = 0; disk < n; disk++)
+        if (r->degraded_mask & (1u << disk)) {
+            if (nd == m)
+                return -EIO;
+            deg[nd++] = disk;
+        }
+    for (uint32_t i = 0; i < count; i++) {
+        const uint64_t s = first + i;
+        int p, q;
+        draid_raid_parity_chunks(r, s, &p, &q);
+        for (int t = 0; t < 2; t++) {
+            uint8_t v = DRAID_EC_FAIL_NONE;
+            if (t < nd) {
+                const int d = draid_raid_disk_data_index(r, s, deg[t]);
+                v = (uint8_t)(d >= 0 ? d : (deg[t] == p ? k : k + 1));
+            }
+            fail[2 * (size_t)i + t] = v;
+        }
+    }
+    return 0;
+}
+
+int draid_raid_strip_table(const struct draid_raid *r, uint64_t first, uint32_t count,
+                           void *const *disk_base, uint64_t disk_first, void **table)
+{
+    if (!r || !disk_base || !table || first < disk_first)
+        return -EINVAL;
+    const int n = r->num_base_bdevs, m = r->max_degraded, k = n - m;
+    const uint64_t sb = (uint64_t)r->strip_size * r->blocklen;
+    for (uint32_t i = 0; i < count; i++) {
+        const uint64_t s = first + i;
+        int p, q;
+        draid_raid_parity_chunks(r, s, &p, &q);
+        for (int j = 0; j < n; j++) {
+            const int disk = j < k ? draid_raid_data_disk(r, s, j) : (j == k ? p : q);
+            table[(size_t)i * n + j] = (uint8_t *)disk_base[disk] + (s - disk_first) * sb;
+        }
+    }
+    return 0;
+}

@@ -161,6 +161,26 @@ int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
                            int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
                            int *nreads);
 
+/* Disk-level failures to stripe-level kernel input, for batched degraded reads
+ * and for rebuilding a failed disk (the rotation of raid5.c:1006-1007 gives a
+ * disk a different role -- data index, P or Q -- in every stripe).
+ *
+ * draid_raid_fail_table: fail[2*i], fail[2*i+1] = the isa-l indices (data
+ * 0..k-1, P = k, Q = k+1) of stripe first+i's strips on the disks in
+ * r->degraded_mask, DRAID_EC_FAIL_NONE-padded -- the `fail` array of
+ * draid_ec_reconstruct.  -EIO if more disks are degraded than the level
+ * tolerates.
+ *
+ * draid_raid_strip_table: the pointer table of draid_ec_stripe_batch for stripes
+ * [first, first+count) when base disk d's blocks start at disk_base[d] (disks in
+ * HBM, or staging regions mirroring them): strip j of stripe s (isa-l order) at
+ * disk_base[disk(s, j)] + (s - disk_first) * strip bytes, where disk_first is the
+ * stripe at each disk_base.  Host memory; copy it to the device for the call. */
+int draid_raid_fail_table(const struct draid_raid *r, uint64_t first, uint32_t count,
+                          uint8_t *fail);
+int draid_raid_strip_table(const struct draid_raid *r, uint64_t first, uint32_t count,
+                           void *const *disk_base, uint64_t disk_first, void **table);
+
 /* Stripe assembly of raid5_simple (raid5_submit_write_request,
  * raid5_simple.c:347-423): with the bdev layer splitting writes at strip
  * boundaries, a full-stripe write arrives as k strip-sized child I/Os on a

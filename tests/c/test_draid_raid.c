@@ -187,6 +187,54 @@ static void test_stripe_asm(void)
     CHECK(draid_raid_asm_add(&r, &a, (s + 1) * r.stripe_blocks, 8, &one, 1) == 0);
 }
 
+/* Disk failures -> per-stripe failure pairs and the rotated pointer table. */
+static void test_fail_table(void)
+{
+    for (int lvl = 5; lvl <= 6; lvl++) {
+        struct draid_raid r;
+        const int n = lvl == 5 ? 5 : 10;
+        CHECK(draid_raid_start(&r, lvl, n, 4096, 16, 16 * 64) == 0);
+        const int m = r.max_degraded, k = n - m;
+        uint8_t f[2 * 40];
+        r.degraded_mask = 0;
+        CHECK(draid_raid_fail_table(&r, 3, 40, f) == 0);
+        for (int i = 0; i < 80; i++)
+            CHECK(f[i] == DRAID_EC_FAIL_NONE);
+        const int d0 = 1, d1 = n - 2;
+        r.degraded_mask = (1u << d0) | (m == 2 ? 1u << d1 : 0);
+        CHECK(draid_raid_fail_table(&r, 3, 40, f) == 0);
+        for (int i = 0; i < 40; i++) {
+            int p, q;
+            draid_raid_parity_chunks(&r, 3 + (uint64_t)i, &p, &q);
+            const int want0 = d0 == p ? k : d0 == q ? k + 1 : draid_raid_disk_data_index(&r, 3 + (uint64_t)i, d0);
+            CHECK(f[2 * i] == want0);
+            if (m == 2) {
+                const int want1 = d1 == p ? k : d1 == q ? k + 1 : draid_raid_disk_data_index(&r, 3 + (uint64_t)i, d1);
+                CHECK(f[2 * i + 1] == want1);
+            } else {
+                CHECK(f[2 * i + 1] == DRAID_EC_FAIL_NONE);
+            }
+        }
+        r.degraded_mask = (1u << (m + 1)) - 1;
+        CHECK(draid_raid_fail_table(&r, 0, 4, f) == -EIO);
+        /* pointer table: strip j of stripe s on its rotated disk at (s - first) strips */
+        static uint8_t disks[10][4];
+        void *base[10];
+        for (int d = 0; d < n; d++)
+            base[d] = disks[d];
+        void *tab[10 * 6];
+        CHECK(draid_raid_strip_table(&r, 7, 6, base, 5, tab) == 0);
+        for (int i = 0; i < 6; i++)
+            for (int j = 0; j < n; j++) {
+                int p, q;
+                draid_raid_parity_chunks(&r, 7 + (uint64_t)i, &p, &q);
+                const int disk = j < k ? draid_raid_data_disk(&r, 7 + (uint64_t)i, j) : (j == k ? p : q);
+                CHECK(tab[i * n + j] == (uint8_t *)base[disk] + (uint64_t)(2 + i) * 16 * 4096);
+            }
+        CHECK(draid_raid_strip_table(&r, 4, 1, base, 5, tab) == -EINVAL);
+    }
+}
+
 /* Stripe cache and request queue (raid5.c:1047-1131, 485-521). */
 static void test_stripe_cache(void)
 {
@@ -611,12 +659,97 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
            rebuilt, refused, g_fail ? "FAIL" : "ok");
 }
 
+/* Rebuild of failed disks held in device memory: encode every stripe of an
+ * array through the rotated pointer table, erase one (or two) disks, rebuild them
+ * with one batched reconstruct driven by the per-stripe failure table. */
+static void run_rebuild(int lvl, int n, uint32_t strip_kb, uint64_t nstripes)
+{
+    struct draid_raid r;
+    const uint32_t strip = strip_kb * 1024 / 4096;
+    CHECK(draid_raid_start(&r, lvl, n, 4096, strip, strip * nstripes) == 0);
+    const int m = r.max_degraded, k = n - m;
+    const size_t sb = (size_t)strip * 4096, db = sb * nstripes;
+    void *st;
+    HIPOK(draid_ec_stream_create(&st));
+    uint8_t *disk[DRAID_RAID_MAX_BASE], *hd[DRAID_RAID_MAX_BASE];
+    uint8_t *zero = calloc(1, db), *tmp = malloc(db);
+    for (int d = 0; d < n; d++) {
+        HIPOK(draid_ec_device_alloc((void **)&disk[d], db));
+        hd[d] = malloc(db);
+        orc_fill_splitmix(hd[d], db, 0x5eed + (uint64_t)d); /* data, and garbage parity */
+        HIPOK(draid_ec_memcpy_async(disk[d], hd[d], db, 0, st));
+    }
+    void **tab = malloc(sizeof(void *) * n * nstripes), **dtab;
+    uint8_t *fail = malloc(2 * nstripes), *dfail;
+    HIPOK(draid_ec_device_alloc((void **)&dtab, sizeof(void *) * n * nstripes));
+    HIPOK(draid_ec_device_alloc((void **)&dfail, 2 * nstripes));
+    CHECK(draid_raid_strip_table(&r, 0, (uint32_t)nstripes, (void *const *)disk, 0, tab) == 0);
+    HIPOK(draid_ec_memcpy_async(dtab, tab, sizeof(void *) * n * nstripes, 0, st));
+    draid_ec_stripe_batch b = {(uint32_t)k, (uint32_t)m, sb, (uint32_t)nstripes, 0, dtab};
+    HIPOK(draid_ec_encode(&b, st));
+    for (int d = 0; d < n; d++)
+        HIPOK(draid_ec_memcpy_async(hd[d], disk[d], db, 1, st));
+    HIPOK(draid_ec_stream_synchronize(st));
+    /* parity on the disks == oracle, for a sample of stripes */
+    uint8_t *ref = malloc(2 * sb);
+    for (uint64_t s = 0; s < nstripes; s += 1 + nstripes / 7) {
+        int p, q;
+        draid_raid_parity_chunks(&r, s, &p, &q);
+        void *vec[DRAID_RAID_MAX_BASE];
+        for (int j = 0; j < k; j++)
+            vec[j] = hd[draid_raid_data_disk(&r, s, j)] + s * sb;
+        vec[k] = ref;
+        vec[k + 1] = ref + sb;
+        CHECK((m == 1 ? orc_xor_gen(k + 1, (int)sb, vec) : orc_pq_gen(k + 2, (int)sb, vec)) == 0);
+        CHECK(cmp_host(hd[p] + s * sb, ref, sb));
+        if (m == 2)
+            CHECK(cmp_host(hd[q] + s * sb, ref + sb, sb));
+    }
+    /* fail every disk alone, and (RAID6) a few pairs: erase, rebuild, compare */
+    int sets = 0;
+    for (int f0 = 0; f0 < n; f0++)
+        for (int f1 = (m == 2 ? f0 + 1 : n); f1 <= n; f1 += (m == 2 ? 3 : 1)) {
+            r.degraded_mask = (1u << f0) | (f1 < n ? 1u << f1 : 0);
+            CHECK(draid_raid_fail_table(&r, 0, (uint32_t)nstripes, fail) == 0);
+            HIPOK(draid_ec_memcpy_async(dfail, fail, 2 * nstripes, 0, st));
+            HIPOK(draid_ec_memcpy_async(disk[f0], zero, db, 0, st));
+            if (f1 < n)
+                HIPOK(draid_ec_memcpy_async(disk[f1], zero, db, 0, st));
+            HIPOK(draid_ec_reconstruct(&b, dfail, st));
+            for (int t = 0; t < 2; t++) {
+                const int f = t ? f1 : f0;
+                if (f >= n)
+                    continue;
+                HIPOK(draid_ec_memcpy_async(tmp, disk[f], db, 1, st));
+                HIPOK(draid_ec_stream_synchronize(st));
+                CHECK(cmp_host(tmp, hd[f], db));
+            }
+            sets++;
+        }
+    r.degraded_mask = 0;
+    printf("  rebuild raid%d n=%d strip=%uKiB stripes=%llu: %d failure sets %s\n", lvl, n, strip_kb,
+           (unsigned long long)nstripes, sets, g_fail ? "FAIL" : "ok");
+    for (int d = 0; d < n; d++) {
+        draid_ec_device_free(disk[d]);
+        free(hd[d]);
+    }
+    draid_ec_device_free(dtab);
+    draid_ec_device_free(dfail);
+    draid_ec_stream_destroy(st);
+    free(tab);
+    free(fail);
+    free(zero);
+    free(tmp);
+    free(ref);
+}
+
 int main(int argc, char **argv)
 {
     const int cpu_only = argc > 1 && strcmp(argv[1], "--cpu-only") == 0;
     test_geometry();
     test_mapping();
     test_stripe_asm();
+    test_fail_table();
     test_stripe_cache();
     test_stripe_cache_threads();
     printf("host logic: %s\n", g_fail ? "FAIL" : "ok");
@@ -625,6 +758,9 @@ int main(int argc, char **argv)
                               {6, 4, 512, 4},  {6, 6, 4096, 64}, {6, 10, 4096, 64}, {6, 18, 4096, 4}};
         for (unsigned i = 0; i < sizeof(cfg) / sizeof(cfg[0]); i++)
             run_array(cfg[i][0], cfg[i][1], (uint32_t)cfg[i][2], (uint32_t)cfg[i][3]);
+        run_rebuild(5, 5, 64, 40);
+        run_rebuild(6, 10, 64, 30);
+        run_rebuild(6, 18, 16, 37);
     }
     printf("%s (%d failures)\n", g_fail ? "FAIL" : "PASS", g_fail);
     return g_fail ? 1 : 0;
