@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--layouts", default="stripe_major,stripe_major_gap256,stripe_major_gap4096,strip_major")
     ap.add_argument("--variants", default="0,1,2,8,10,11,12")
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--fail-order", default="random", choices=["random", "sorted", "fixed"],
+                    help="per-stripe failure pairs: seeded random (bench), the same pairs "
+                         "sorted so neighbouring stripes share one, or one pair everywhere")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.json"))
     args = ap.parse_args()
 
@@ -116,7 +119,12 @@ def main():
     m = 1 if k == 4 else 2
     probes = probe(torch, dev, (k + m) * S * B, args.rounds, args.iters) if args.probe else []
     fgen = bench.failure_pairs if args.failures == "dual" else bench.failure_single
-    fail = torch.from_numpy(fgen(B, k, 0x1234).reshape(-1)).to(dev)
+    fnp0 = fgen(B, k, 0x1234)
+    if args.fail_order == "sorted":
+        fnp0 = fnp0[np.lexsort((fnp0[:, 1], fnp0[:, 0]))].copy()
+    elif args.fail_order == "fixed":
+        fnp0 = np.repeat(fnp0[:1], B, axis=0).copy()
+    fail = torch.from_numpy(fnp0.reshape(-1)).to(dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     layouts = {}
@@ -133,7 +141,7 @@ def main():
         ec.encode(batch, sh)
         torch.cuda.synchronize(dev)
         good = view.clone()
-        fnp = fgen(B, k, 0x1234)
+        fnp = fnp0
         rows = torch.arange(B, device=dev)
         for v in variants:
             ec.set_variant(v)
