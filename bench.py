@@ -118,25 +118,38 @@ def cpu_baseline(k: int, m: int, S: int, failures: str, seconds: float, threads:
     AVX-512 (+GFNI affine) restatement of isa-l's x86 kernels when the host has
     them (oracle/isal_simd.c), else the scalar one; also times one core."""
     import oracle
-    B = 64
-    buf = np.frombuffer(np.random.default_rng(1).bytes((k + m) * S * B), np.uint8).copy()
-    fail = (failure_pairs if failures == "dual" else failure_single)(B, k, 7).reshape(-1)
     simd = oracle.simd_available()
 
-    def run(nthr, secs):
-        el, passes = oracle.bench_encode_reconstruct(buf, k, m, S, B, S, (k + m) * S, fail, True,
-                                                     nthr, secs, simd=simd)
-        return (2.0 * k * S * B * passes / el / GIB, passes, el) if el > 0 else (None, 0, el)
+    def sample(nstripes):
+        buf = np.frombuffer(np.random.default_rng(1).bytes((k + m) * S * nstripes), np.uint8).copy()
+        fail = (failure_pairs if failures == "dual" else failure_single)(nstripes, k, 7)
+        return buf, fail.reshape(-1)
 
-    value, passes, el = run(threads, seconds)
+    def run(buf, fail, nstripes, nthr, secs):
+        el, passes = oracle.bench_encode_reconstruct(buf, k, m, S, nstripes, S, (k + m) * S, fail,
+                                                     True, nthr, secs, simd=simd)
+        return (2.0 * k * S * nstripes * passes / el / GIB, passes, el) if el > 0 else (None, 0, el)
+
+    B = 64  # cache-resident (tens of MiB): the CPU's best case
+    buf, fail = sample(B)
+    value, passes, el = run(buf, fail, B, threads, seconds)
     if value is None:
         return {"value": None, "error": "oracle bench failed"}
-    one, _, _ = run(1, max(1.0, seconds / 4))
+    one, _, _ = run(buf, fail, B, 1, max(1.0, seconds / 4))
+    # the same work streaming from DRAM, as the full-size workload would run on the host
+    B2 = max(64, (1 << 30) // ((k + m) * S))
+    del buf
+    buf2, fail2 = sample(B2)
+    dram, passes2, el2 = run(buf2, fail2, B2, threads, max(1.0, seconds / 2))
+    del buf2
     impl = ("AVX-512BW + GFNI restatement of isa-l's pq_gen_avx512 / gf_vect_mul (affine "
             "constant multiply)" if simd else
             "64-bit SWAR restatement of isa-l pq_gen_base + nibble-table gf_vect_mul, -O3 -mavx2")
     return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "single_core_value": round(one, 3) if one else None,
+            "dram_resident_value": round(dram, 3) if dram else None,
+            "dram_resident_sample": f"{B2} stripes ({(k + m) * S * B2 >> 20} MiB), {passes2} "
+                                    f"passes in {el2:.1f}s, {threads} pthreads",
             "sample": f"{B} stripes x {k}+{m} x {S // 1024} KiB, encode + {failures}-failure "
                       f"reconstruct, {passes} passes in {el:.1f}s, C oracle ({impl}), "
                       f"{threads} pthreads"}

@@ -11,7 +11,7 @@ for q in 32 1; do
   cp gpurun_out/config1_cpu.json gpurun_out/config1_cpu_q$q.json
 done
 : > gpurun_out/config1_gpu.jsonl
-for qg in "32 1" "32 2" "32 4" "128 4"; do
+for qg in "1 1" "32 1" "32 2" "32 4" "128 4"; do
   set -- $qg
   timeout -k 10 120 tools/c/bdevperf_gpu ${SECS:-10} $1 $2 >> gpurun_out/config1_gpu.jsonl 2> gpurun_out/config1_gpu.err || { cat gpurun_out/config1_gpu.err; exit 1; }
   tail -1 gpurun_out/config1_gpu.jsonl
