@@ -270,11 +270,35 @@ int flush_piece(draid_ec_ctx* c, const Group& g, size_t s0, size_t s1)
 
 // Launches a group in pieces of about kPieceBytes of descriptors, so the upload
 // of piece i+1 overlaps the kernel of piece i.
+// A group of one segment whose pointers fit in the kernel arguments (the
+// low-queue-depth case: one stripe per poll) launches the single-stripe kernel
+// directly -- no descriptor upload, no ring slot, no cross-stream event.
+int flush_single(draid_ec_ctx* c, Group& g)
+{
+    draid::ArgPtrTable args;
+    memset(&args, 0, sizeof(args));
+    const uint32_t n = g.k + g.m;
+    for (uint32_t j = 0; j < n; ++j)
+        args.p[j] = static_cast<const uint8_t*>(g.ptrs[j]);
+    hipError_t e;
+    if (g.op == 0)
+        e = draid::launch_encode(g.k, g.m, g.len[0], 1, nullptr, &args, c->stream);
+    else
+        e = draid::launch_reconstruct(g.k, g.m, g.len[0], 1, nullptr, &args, nullptr, g.fail[0],
+                                      g.fail[1], c->stream);
+    g.ptrs.clear();
+    g.len.clear();
+    g.fail.clear();
+    return e == hipSuccess ? 0 : ctx_fail(e, "launch (single segment)");
+}
+
 int flush_group(draid_ec_ctx* c, Group& g)
 {
     const size_t nseg = g.len.size();
     if (nseg == 0)
         return 0;
+    if (nseg == 1 && g.op != 2 && g.k + g.m <= static_cast<uint32_t>(draid::kMaxArgPtrs))
+        return flush_single(c, g);
     const size_t per_seg = (g.k + g.m) * sizeof(void*) + sizeof(uint32_t) + 2 * sizeof(uint32_t);
     const size_t piece = std::max<size_t>(kMinPieceSegments, kPieceBytes / per_seg);
     int rc = 0;

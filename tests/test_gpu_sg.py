@@ -244,3 +244,40 @@ def test_sg_adjacent_iovecs_merge(ec):
         strip = np.concatenate([scat[j * (L + 5 * gap) + a + i * gap:][:ln]
                                 for i, (a, ln) in enumerate(pieces)])
         assert (strip == ref[j]).all()
+
+
+@pytest.mark.parametrize("k,m,L", [(8, 2, 65536), (4, 1, 4096 + 16), (14, 2, 999), (30, 2, 2048)])
+def test_sg_single_segment_flush(ec, k, m, L):
+    """One contiguous stripe per flush (the queue-depth-1 case) launches the
+    single-stripe kernel with its pointers in the kernel arguments; a many-segment
+    flush queued before it on the same context is ordered ahead of it."""
+    n = k + m
+    rng = np.random.default_rng(L + k)
+    host = np.zeros((3, n, L), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (3, k, L), dtype=np.uint8)
+    ref = host.copy()
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, 3, L, n * L) == 0
+    dbuf = torch.from_numpy(host).to(DEV)
+    base = dbuf.data_ptr()
+    ctx = ec.Ctx()
+    try:
+        # stripe 0 as two segments (a split iovec), then stripes 1 and 2 alone
+        half = L // 2
+        strips0 = [[(base + j * L, half), (base + j * L + half + 64 * 0, L - half)] for j in range(n)]
+        ctx.encode_sg(k, m, strips0, L)
+        ctx.flush()
+        for s in (1, 2):
+            ctx.encode_sg(k, m, [[(base + (s * n + j) * L, L)] for j in range(n)], L)
+            ctx.flush()
+        ctx.synchronize()
+        assert (dbuf.cpu().numpy() == ref).all()
+        # single-segment rebuild of the worst case the level allows
+        lost = [1, k] if m == 2 else [k - 1]
+        for j in lost:
+            dbuf[2, j] = 0xA5
+        ctx.reconstruct_sg(k, m, [[(base + (2 * n + j) * L, L)] for j in range(n)], L, lost)
+        ctx.flush()
+        ctx.synchronize()
+        assert (dbuf.cpu().numpy() == ref).all()
+    finally:
+        ctx.close()
