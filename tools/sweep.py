@@ -34,7 +34,9 @@ VARIANTS = {0: "default (64 lanes U1)", 1: "U2", 2: "512 lanes U1", 3: "128 lane
             28: "st sc0 nt", 29: "ld buffer nt", 30: "ld sc1 nt", 31: "ld sc0 sc1 nt",
             32: "ld sc0 nt", 33: "ld sc1 st sc1", 34: "ld buf nt st sc1 nt",
             35: "ld buf nt st buf nt", 36: "ld buf nt st sc1", 37: "ld sc0sc1nt st sc1nt",
-            38: "XCD-aware, enc policy", 39: "XCD-aware, rec policy"}
+            38: "XCD-aware, enc policy", 39: "XCD-aware, rec policy",
+            40: "enc G16 diagonal", 41: "enc G16 same chunk", 42: "enc G4 diagonal",
+            43: "enc G4 same chunk", 44: "rec G16 diagonal", 45: "rec G4 diagonal"}
 
 
 def probe(torch, dev, nbytes, rounds, iters):
