@@ -183,12 +183,11 @@ int draid_raid_stripe_write(const struct draid_raid *r, draid_ec_ctx *ctx,
     return 0;
 }
 
-int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ctx,
-                                    uint64_t stripe, void *const *chunk_buf,
-                                    struct draid_base_io *reads, int *nreads)
+/* Whole-stripe degraded read: reads (when `reads` is given) and the reconstruct
+ * (when `ctx` is given) of stripe `stripe`. */
+static int degraded_read(const struct draid_raid *r, draid_ec_ctx *ctx, uint64_t stripe,
+                         void *const *chunk_buf, struct draid_base_io *reads, int *nreads)
 {
-    if (!r || !ctx || !chunk_buf || !reads || !nreads)
-        return -EINVAL;
     const int n = r->num_base_bdevs, m = r->max_degraded, k = n - m;
     const uint64_t sb = (uint64_t)r->strip_size * r->blocklen;
     int p, q, fail[2], nfail = 0, nr = 0;
@@ -201,6 +200,8 @@ int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ct
             fail[nfail++] = d >= 0 ? d : (disk == p ? k : k + 1);
             continue;
         }
+        if (!reads)
+            continue;
         struct draid_base_io *rd = &reads[nr++];
         rd->disk = disk;
         rd->offset_blocks = stripe << r->strip_size_shift;
@@ -209,8 +210,9 @@ int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ct
         rd->iov[0].iov_base = chunk_buf[disk];
         rd->iov[0].iov_len = sb;
     }
-    *nreads = nr;
-    if (nfail == 0)
+    if (nreads)
+        *nreads = nr;
+    if (nfail == 0 || !ctx)
         return 0;
     struct iovec v[DRAID_RAID_MAX_BASE];
     const struct iovec *lists[DRAID_RAID_MAX_BASE];
@@ -225,6 +227,23 @@ int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ct
     int rc = draid_ec_ctx_reconstruct_sg(ctx, (uint32_t)k, (uint32_t)m, lists, cnts, NULL, sb,
                                          nfail, fail);
     return rc > 0 ? -EINVAL : rc;
+}
+
+int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                    uint64_t stripe, void *const *chunk_buf,
+                                    struct draid_base_io *reads, int *nreads)
+{
+    if (!r || !chunk_buf || !reads || !nreads)
+        return -EINVAL;
+    return degraded_read(r, ctx, stripe, chunk_buf, reads, nreads);
+}
+
+int draid_raid_stripe_degraded_rebuild(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                       uint64_t stripe, void *const *chunk_buf)
+{
+    if (!r || !ctx || !chunk_buf)
+        return -EINVAL;
+    return degraded_read(r, ctx, stripe, chunk_buf, NULL, NULL);
 }
 
 /* ------------------------------------------------------------ partial writes */
@@ -504,13 +523,12 @@ static int range_list(const struct draid_raid *r, const struct draid_stripe_req 
     return n;
 }
 
-int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
-                           const struct draid_stripe_req *req, const struct iovec *iov,
-                           int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
-                           int *nreads)
+/* Ranged read: the base reads (when `reads` is given) and the reconstruct of the
+ * lost requested range (when `ctx` is given). */
+static int ranged_read(const struct draid_raid *r, draid_ec_ctx *ctx,
+                       const struct draid_stripe_req *req, const struct iovec *iov, int iovcnt,
+                       void *const *chunk_buf, struct draid_base_io *reads, int *nreads)
 {
-    if (!r || !ctx || !req || !iov || !chunk_buf || !reads || !nreads)
-        return -EINVAL;
     const int n = r->num_base_bdevs, m = r->max_degraded, k = n - m;
     const uint64_t s = req->stripe_index, lba = s << r->strip_size_shift;
     const int pdisk = req->p_disk, qdisk = req->q_disk;
@@ -532,13 +550,14 @@ int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
     }
     int nr = 0, rc;
     if (hi <= lo) { /* nothing to rebuild: plain reads (raid5.c:933-945) */
-        for (int d = req->first_data; d <= req->last_data; d++) {
+        for (int d = req->first_data; reads && d <= req->last_data; d++) {
             if (!req->chunk[draid_raid_data_disk(r, s, d)].req_blocks)
                 continue;
             if ((rc = read_request(r, req, d, iov, iovcnt, &reads[nr++])) < 0)
                 return rc;
         }
-        *nreads = nr;
+        if (nreads)
+            *nreads = nr;
         return 0;
     }
     if (ndeg > m)
@@ -566,7 +585,7 @@ int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
             return cnt;
         lists[j] = lv[j];
         cnts[j] = cnt;
-        if ((r->degraded_mask & (1u << disk)) || (disk == qdisk && !needq))
+        if (!reads || (r->degraded_mask & (1u << disk)) || (disk == qdisk && !needq))
             continue;
         if (d >= 0 && c->req_blocks && (rc = read_request(r, req, d, iov, iovcnt, &reads[nr++])) < 0)
             return rc;
@@ -578,10 +597,32 @@ int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
         if (u1 < hi)
             add_io(&reads[nr++], disk, lba, u1, hi - u1, chunk_buf[disk], r->blocklen);
     }
-    *nreads = nr;
+    if (nreads)
+        *nreads = nr;
+    if (!ctx)
+        return 0;
     rc = draid_ec_ctx_reconstruct_sg(ctx, (uint32_t)k, (uint32_t)m, lists, cnts, NULL,
                                      (hi - lo) * r->blocklen, nfail, fail);
     return rc > 0 ? -EINVAL : rc;
+}
+
+int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
+                           const struct draid_stripe_req *req, const struct iovec *iov,
+                           int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
+                           int *nreads)
+{
+    if (!r || !req || !iov || !chunk_buf || !reads || !nreads)
+        return -EINVAL;
+    return ranged_read(r, ctx, req, iov, iovcnt, chunk_buf, reads, nreads);
+}
+
+int draid_raid_stripe_read_rebuild(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                   const struct draid_stripe_req *req, const struct iovec *iov,
+                                   int iovcnt, void *const *chunk_buf)
+{
+    if (!r || !ctx || !req || !iov || !chunk_buf)
+        return -EINVAL;
+    return ranged_read(r, ctx, req, iov, iovcnt, chunk_buf, NULL, NULL);
 }
 
 /* ------------------------------------------------------------ stripe assembly */

@@ -140,6 +140,13 @@ int draid_raid_stripe_write_partial(const struct draid_raid *r, draid_ec_ctx *ct
 int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ctx,
                                     uint64_t stripe, void *const *chunk_buf,
                                     struct draid_base_io *reads, int *nreads);
+/* Two-phase form for base reads that complete asynchronously (a real module):
+ * draid_raid_stripe_degraded_read with ctx = NULL lists the reads only; once they
+ * are in, draid_raid_stripe_degraded_rebuild queues the reconstruct on ctx.  (With
+ * a ctx the one call does both: right when the reads are ordered before the
+ * flush, e.g. copies on the ctx's stream.) */
+int draid_raid_stripe_degraded_rebuild(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                       uint64_t stripe, void *const *chunk_buf);
 
 /* Ranged read of one stripe request (raid5_stripe_read, raid5.c:869-946, and
  * raid5_complete_reconstructed_stripe_request, raid5.c:544-594, generalised to
@@ -153,13 +160,20 @@ int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ct
  * request covers are read into the parent iovecs, the rest into chunk_buf, and
  * the kernel gathers R from both: no copy pass.  Lost requested ranges are
  * rebuilt straight into the parent iovecs.  chunk_buf[disk] are strip-sized
- * scratch buffers; reads[] must hold 3 * n entries.  Once the base reads are
- * in, draid_ec_ctx_flush + query/synchronize finish the request.  -EIO if a
- * rebuild is needed and more disks are degraded than the level tolerates. */
+ * scratch buffers; reads[] must hold 3 * n entries.  With a ctx the
+ * reconstruct is queued at once (the reads must then reach memory before the
+ * flush runs); see the two-phase form below.  -EIO if a rebuild is needed and more
+ * disks are degraded than the level tolerates. */
 int draid_raid_stripe_read(const struct draid_raid *r, draid_ec_ctx *ctx,
                            const struct draid_stripe_req *req, const struct iovec *iov,
                            int iovcnt, void *const *chunk_buf, struct draid_base_io *reads,
                            int *nreads);
+/* Two-phase form (as for the whole-stripe read): draid_raid_stripe_read with
+ * ctx = NULL plans the reads; after they complete, draid_raid_stripe_read_rebuild
+ * with the same arguments queues the reconstruct of the lost requested range. */
+int draid_raid_stripe_read_rebuild(const struct draid_raid *r, draid_ec_ctx *ctx,
+                                   const struct draid_stripe_req *req, const struct iovec *iov,
+                                   int iovcnt, void *const *chunk_buf);
 
 /* Disk-level failures to stripe-level kernel input, for batched degraded reads
  * and for rebuilding a failed disk (the rotation of raid5.c:1006-1007 gives a

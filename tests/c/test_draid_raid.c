@@ -531,11 +531,16 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
             int nr = 0;
             for (int d = 0; d < n; d++)
                 d2d(chunk[d], junk, sb, st); /* degraded chunks start as garbage */
-            CHECK(draid_raid_stripe_degraded_read(&r, ctx, s, (void *const *)chunk, rd, &nr) == 0);
+            /* odd f0: the two-phase form (plan, base reads, then the rebuild) */
+            const int two = f0 & 1;
+            CHECK(draid_raid_stripe_degraded_read(&r, two ? NULL : ctx, s, (void *const *)chunk, rd,
+                                                  &nr) == 0);
             CHECK(nr == n - (f1 < n ? 2 : 1));
             for (int i = 0; i < nr; i++) /* fake base reads */
                 d2d(rd[i].iov[0].iov_base, disk[rd[i].disk] + rd[i].offset_blocks * blocklen, sb,
                     st);
+            if (two)
+                CHECK(draid_raid_stripe_degraded_rebuild(&r, ctx, s, (void *const *)chunk) == 0);
             HIPOK(draid_ec_ctx_flush(ctx));
             HIPOK(draid_ec_ctx_synchronize(ctx));
             for (int d = 0; d < n; d++) {
@@ -602,8 +607,9 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
                 d2d(chunk[d], junk, sb, st);
             d2d(ubuf, ujunk, nb, st);
             int nio = -1;
-            const int rc = draid_raid_stripe_read(&r, ctx, &q, uiov, 3, (void *const *)chunk, rio,
-                                                  &nio);
+            const int two = t & 1; /* odd t: plan the reads, rebuild after they are in */
+            const int rc = draid_raid_stripe_read(&r, two ? NULL : ctx, &q, uiov, 3,
+                                                  (void *const *)chunk, rio, &nio);
             nreq++;
             if (lost_req && nd > m) {
                 CHECK(rc == -EIO);
@@ -626,6 +632,9 @@ static void run_array(int lvl, int n, uint32_t blocklen, uint32_t strip_kb)
                 }
                 CHECK(o == (size_t)(rio[i].offset_blocks + rio[i].num_blocks) * blocklen);
             }
+            if (two)
+                CHECK(draid_raid_stripe_read_rebuild(&r, ctx, &q, uiov, 3, (void *const *)chunk) ==
+                      0);
             HIPOK(draid_ec_ctx_flush(ctx));
             HIPOK(draid_ec_ctx_synchronize(ctx));
             HIPOK(draid_ec_memcpy_async(hr, ubuf, nb, 1, st));
