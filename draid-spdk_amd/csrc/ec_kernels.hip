@@ -713,8 +713,8 @@ __global__ __launch_bounds__(C::NTHR) void k_update_work(const uint8_t* const* t
             W dp = W(0), dq = W(0);
             int prev = -1;
             for (uint32_t t = 0; t < nd; ++t) {
-                const W delta = MW::template ld<3>(row[2 * t], i) ^
-                                MW::template ld<3>(row[2 * t + 1], i);
+                const W delta = MW::template ld<C::POL>(row[2 * t], i) ^
+                                MW::template ld<C::POL>(row[2 * t + 1], i);
                 dp ^= delta;
                 if constexpr (M == 2) {
                     const int e = ex[t];
@@ -724,11 +724,11 @@ __global__ __launch_bounds__(C::NTHR) void k_update_work(const uint8_t* const* t
                     prev = e;
                 }
             }
-            MW::template st<3>(pP, i, MW::template ld<3>(pP, i) ^ dp);
+            MW::template st<C::POL>(pP, i, MW::template ld<C::POL>(pP, i) ^ dp);
             if constexpr (M == 2) {
                 for (int g = prev; g > 0; --g)
                     dq = gf_mul2(dq);
-                MW::template st<3>(pQ, i, MW::template ld<3>(pQ, i) ^ dq);
+                MW::template st<C::POL>(pQ, i, MW::template ld<C::POL>(pQ, i) ^ dq);
             }
         };
         if ((acc & 15u) == 0) {
@@ -1192,7 +1192,7 @@ hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* tab
                               const uint8_t* exps, const uint32_t* seg_len, const void* work,
                               uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
-    using C = CfgDefault<1>;
+    using C = EncCfg<1>;  // buffer nt loads, write-through nt stores
     if (nwork == 0)
         return hipSuccess;
     const WorkSrc ws = work_src<C>(seg_len, work, ulen);

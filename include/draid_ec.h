@@ -177,7 +177,9 @@ int draid_ec_ctx_update_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m, uint32_t n
                            const int *par_cnt, size_t len);
 
 /* Launch everything queued (non-blocking; blocks only if the descriptor ring
- * is 4 flushes behind).  draid_ec_ctx_query: 0 idle, 1 running, < 0 error. */
+ * is 4 flushes behind).  The context's stream is non-blocking: it does not wait
+ * for work on other streams, so every queued buffer must hold its data when
+ * flush is called.  draid_ec_ctx_query: 0 idle, 1 running, < 0 error. */
 int draid_ec_ctx_flush(draid_ec_ctx *ctx);
 int draid_ec_ctx_query(draid_ec_ctx *ctx);
 int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);

@@ -33,6 +33,7 @@ def test_rmw_update_matches_reencode(ec, k, m, L, B):
     stripes = torch.from_numpy(host.copy()).to(DEV)
     newdata = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).to(DEV)
     olddata = stripes[:, :k].clone()           # the RMW preread of the touched chunks
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
     expect = host.copy()
     ctx = ec.Ctx()
     try:

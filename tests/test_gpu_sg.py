@@ -105,6 +105,7 @@ def test_sg_encode_and_reconstruct(ec, k, m, L, B, prefix):
             for j in f:
                 pool.scatter(erased, s, j, np.full(L, 0x5A, np.uint8))
         dbuf.copy_(torch.from_numpy(erased))
+        torch.cuda.synchronize()  # torch's stream before the context's own stream
         for s in range(B):
             offs = pool.offsets[s] if prefix else None
             assert ctx.reconstruct_sg(k, m, pool.strips(base, s), L, fails[s], offs) == 0
@@ -172,6 +173,7 @@ def test_sg_uniform_segments(ec, L, piece):
     buf = torch.randint(0, 256, (B, n, L), dtype=torch.uint8, device=DEV, generator=g)
     buf[:, k:] = 0
     base = buf.data_ptr()
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
 
     def strips(s):
         return [[(base + (s * n + j) * L + o, min(piece, L - o)) for o in range(0, L, piece)]
@@ -192,6 +194,7 @@ def test_sg_uniform_segments(ec, L, piece):
         for s, f in enumerate(fails):
             for j in f:
                 buf[s, j] = 0xC3
+        torch.cuda.synchronize()  # torch's stream before the context's own stream
         for s, f in enumerate(fails):
             assert ctx.reconstruct_sg(k, m, strips(s), L, f) == 0
         ctx.flush()
@@ -275,6 +278,7 @@ def test_sg_single_segment_flush(ec, k, m, L):
         lost = [1, k] if m == 2 else [k - 1]
         for j in lost:
             dbuf[2, j] = 0xA5
+        torch.cuda.synchronize()  # torch's stream before the context's own stream
         ctx.reconstruct_sg(k, m, [[(base + (2 * n + j) * L, L)] for j in range(n)], L, lost)
         ctx.flush()
         ctx.synchronize()

@@ -58,6 +58,7 @@ def test_contexts_on_many_threads(ec):
             for _ in range(T)]
     for b in bufs:
         b[:, k:] = 0
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
     errors = []
 
     def worker(t):
