@@ -208,9 +208,11 @@ int draid_gf_vect_mul(int len, unsigned char* tbl, void* src, void* dest)
 
 int draid_recover(int k, int m, int len, void** array, int nfail, const int* fail)
 {
-    if (k < 1 || k > 255 || m < 1 || m > 2 || len < 0 || nfail < 0 || nfail > m || !array ||
+    // failed strip indices travel as bytes with 0xFF = none, so every index
+    // 0 .. k+m-1 must stay below 0xFF
+    if (k < 1 || k + m > 255 || m < 1 || m > 2 || len < 0 || nfail < 0 || nfail > m || !array ||
         (nfail && !fail))
-        return fail_arg("recover needs 1 <= k <= 255, m in {1,2}, nfail <= m");
+        return fail_arg("recover needs k >= 1, k + m <= 255, m in {1,2}, nfail <= m");
     uint8_t f[2] = {DRAID_EC_FAIL_NONE, DRAID_EC_FAIL_NONE};
     for (int i = 0; i < nfail; ++i) {
         if (fail[i] < 0 || fail[i] >= k + m)
@@ -265,6 +267,8 @@ int draid_ec_reconstruct(const draid_ec_stripe_batch* b, const uint8_t* fail, vo
     int rc = check_batch(b);
     if (rc || !b->nstripes || !b->strip_len)
         return rc;
+    if (b->k + b->m > 255)  // failure indices are bytes, 0xFF = none
+        return fail_arg("reconstruct needs k + m <= 255");
     if (!fail)
         return fail_arg("reconstruct: fail table is NULL");
     hipError_t e = draid::launch_reconstruct(
@@ -305,6 +309,8 @@ int draid_ec_reconstruct_strided(const draid_ec_strided_stripes* d, const uint8_
     int rc = check_strided(d);
     if (rc || !d->nstripes || !d->strip_len)
         return rc;
+    if (d->k + d->m > 255)  // failure indices are bytes, 0xFF = none
+        return fail_arg("reconstruct needs k + m <= 255");
     if (!fail)
         return fail_arg("reconstruct: fail table is NULL");
     hipError_t e = draid::launch_reconstruct_strided(

@@ -381,9 +381,9 @@ int draid_ec_ctx_reconstruct_sg(draid_ec_ctx* c, uint32_t k, uint32_t m,
                                 const struct iovec* const* iovs, const int* iovcnt,
                                 const size_t* offset, size_t len, int nfail, const int* fail)
 {
-    if (!c || k < 1 || k > 255 || m < 1 || m > 2 || nfail < 0 || nfail > (int)m ||
+    if (!c || k < 1 || k + m > 255 || m < 1 || m > 2 || nfail < 0 || nfail > (int)m ||
         (nfail && !fail))
-        return ctx_arg("reconstruct_sg needs a ctx, 1 <= k <= 255, m in {1,2}, nfail <= m");
+        return ctx_arg("reconstruct_sg needs a ctx, k >= 1, k + m <= 255, m in {1,2}, nfail <= m");
     uint8_t f[2] = {DRAID_EC_FAIL_NONE, DRAID_EC_FAIL_NONE};
     for (int i = 0; i < nfail; ++i) {
         if (fail[i] < 0 || fail[i] >= (int)(k + m) || (i == 1 && fail[1] == fail[0]))

@@ -274,6 +274,8 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
         return rc;
     if (!fail)
         return draid::fail_arg("host reconstruct: fail table is NULL");
+    if (h->k + h->m > 255)  // failure indices are bytes, 0xFF = none
+        return draid::fail_arg("host reconstruct needs k + m <= 255");
     const uint32_t k = h->k, m = h->m, n = k + m;
     const uint64_t S = h->strip_len;
     if (!(h->flags & DRAID_EC_HOST_STAGED))

@@ -81,6 +81,7 @@ int draid_gf_vect_mul(int len, unsigned char *tbl, void *src, void *dest);
  * raid5.c:544-594 and gf_vect_mul.c:242-347 as one kernel):
  * array = k data pointers, then P (array[k]) and, for m == 2, Q (array[k+1]).
  * The nfail (<= m) strips listed in fail[] are regenerated in place.
+ * k + m <= 255 (every reconstruct call: strip indices are bytes, 0xFF = none).
  * Invalid or unrecoverable failure sets -> 1. */
 int draid_recover(int k, int m, int len, void **array, int nfail, const int *fail);
 

@@ -85,6 +85,13 @@ def test_argument_errors_before_any_launch():
         assert L.draid_ec_encode(C.byref(b), None) == 1, draid_ec.last_error()
     assert L.draid_ec_reconstruct(C.byref(cases[-1]), dummy, None) == 1
     assert "too large" in draid_ec.last_error()
+    # failure indices are bytes with 0xFF = none: reconstructs need k + m <= 255
+    wide = draid_ec.StripeBatch(254, 2, 4096, 1, 0, dummy.value)
+    assert L.draid_ec_reconstruct(C.byref(wide), dummy, None) == 1
+    assert "k + m <= 255" in draid_ec.last_error()
+    arr257 = (C.c_void_p * 257)(*([dummy.value] * 257))
+    f = (C.c_int * 1)(0)
+    assert L.draid_recover(255, 2, 64, arr257, 1, f) == 1
     h = draid_ec.HostStripes(8, 2, 1 << 30, 4096, 0, dummy.value, 1 << 30, 10 << 30)
     assert L.draid_ec_encode_strided(C.byref(h), None) == 1
     assert L.draid_ec_host_encode(C.byref(h), 0) == 1

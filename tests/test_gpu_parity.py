@@ -188,6 +188,65 @@ def test_recover_every_failure_set(ec, k, m):
             assert (host(bufs[j]) == ref[j]).all(), (fail, j)
 
 
+def test_maximum_stripe_width(ec):
+    """The widest stripes the ABI accepts: encode with k = 255 data strips (Q
+    coefficients up to 2^254, pointers through the device scratch table), and
+    reconstruct with k + m = 255 (failure indices are bytes, 0xFF = none) at the
+    ends of the coefficient range, against the oracle; wider reconstructs are
+    rejected."""
+    L = 512 + 32
+    k, m = 255, 2
+    rng = np.random.default_rng(255)
+    data = np.zeros((k + m, L), np.uint8)
+    data[:k] = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    ref = oracle_encode(data[None], k, m)[0]
+    bufs = [dev(data[j]) for j in range(k + m)]
+    assert ec.pq_gen(bufs, L) == 0
+    assert all((host(bufs[j]) == ref[j]).all() for j in range(k + m))
+    assert ec.recover(k, m, L, bufs, [0]) == 1          # k + m = 257 > 255
+    assert ec.recover(254, 2, L, bufs[:256], [0]) == 1  # 256 > 255
+    k, m = 253, 2
+    rng = np.random.default_rng(255)
+    data = np.zeros((k + m, L), np.uint8)
+    data[:k] = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    ref = oracle_encode(data[None], k, m)[0]
+    bufs = [dev(data[j]) for j in range(k + m)]
+    assert ec.pq_gen(bufs, L) == 0
+    assert all((host(bufs[j]) == ref[j]).all() for j in range(k + m))
+    for fail in [(0,), (k - 1,), (0, k - 1), (k - 2, k - 1), (k - 1, k), (0, k + 1), (k, k + 1),
+                 (127, 128)]:
+        for f in fail:
+            bufs[f].fill_(0x3C)
+        assert ec.recover(k, m, L, bufs, list(fail)) == 0
+        for j in range(k + m):
+            assert (host(bufs[j]) == ref[j]).all(), (fail, j)
+
+
+def test_gigabyte_strips_roundtrip(ec):
+    """Strips of 1 GiB + 48 bytes (the 32-bit in-kernel offsets near their range,
+    plus the byte tail) through the batched API: encode, erase two data strips,
+    reconstruct, compare; P checked against an XOR on the device."""
+    k, m, L = 2, 2, (1 << 30) + 48
+    n = k + m
+    buf = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    view = buf.view(n, L)
+    view[:k] = torch.randint(0, 256, (k, L), dtype=torch.uint8, device=DEV, generator=g)
+    table = torch.tensor([buf.data_ptr() + j * L for j in range(n)], dtype=torch.int64, device=DEV)
+    batch = ec.make_batch(k, m, L, 1, table)
+    sh = torch.cuda.current_stream().cuda_stream
+    assert ec.encode(batch, sh) == 0
+    sync()
+    assert torch.equal(view[2], view[0] ^ view[1])
+    good = view[:k].clone()
+    view[:k] = 0
+    fail = torch.tensor([0, 1], dtype=torch.uint8, device=DEV)
+    assert ec.reconstruct(batch, fail, sh) == 0
+    sync()
+    assert torch.equal(view[:k], good)
+
+
 # ------------------------------------------------------------ batched API
 
 CONFIGS = [  # (k, m, strip bytes, stripes) -- BASELINE.json configs at reduced batch
