@@ -367,7 +367,9 @@ int orc_encode_strided(int k, int m, size_t len, uint32_t nstripes,
         return -1;
     for (uint32_t s = 0; s < nstripes; s++) {
         strided_ptrs(k, m, base, strip_stride, stripe_stride, s, ptrs);
-        if (m == 1) {
+        if (m == 1 && k == 1) {
+            memcpy(ptrs[1], ptrs[0], len); /* P = D_0 (xor_gen needs vects >= 3) */
+        } else if (m == 1) {
             int rc = orc_xor_gen(k + 1, (int)len, ptrs);
             if (rc)
                 return rc;

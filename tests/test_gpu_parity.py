@@ -329,6 +329,38 @@ def test_reconstruct_ignores_unrecoverable(ec):
     assert (host(b.strips()) == before).all()
 
 
+@pytest.mark.parametrize("m", [1, 2])
+def test_single_data_strip_and_odd_failure_entries(ec, m):
+    """k = 1 (P and Q are copies of D0), and failure tables with a duplicated index,
+    an out-of-range entry beside a real one, and the real index in the second slot:
+    each stripe rebuilds exactly its one lost strip."""
+    for k, L, B in [(1, 4096 + 5, 4), (6, 2048, 5)]:
+        n = k + m
+        rng = np.random.default_rng(k + 10 * m)
+        data = np.zeros((B, n, L), np.uint8)
+        data[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+        ref = oracle_encode(data, k, m)
+        b = Batch(k, m, L, B, data=data)
+        stream = torch.cuda.current_stream().cuda_stream
+        assert ec.encode(b.batch(ec), stream) == 0
+        sync()
+        assert (host(b.strips()) == ref).all()
+        if k == 1:
+            assert (ref[:, 1] == ref[:, 0]).all()        # P = D0
+            if m == 2:
+                assert (ref[:, 2] == ref[:, 0]).all()    # Q = 2^0 D0
+        lost = [0, k, 0, n - 1, k - 1]
+        rows = [[lost[0], lost[0]], [lost[1], 200], [0xFF, lost[2]], [n + 3, lost[3]],
+                [lost[4], 0xFF]][:B]
+        v = b.strips()
+        for s in range(B):
+            v[s, lost[s]].fill_(0xE1)
+        fail = np.array(rows, np.uint8).reshape(-1)
+        assert ec.reconstruct(b.batch(ec), dev(fail), stream) == 0
+        sync()
+        assert (host(b.strips()) == ref).all(), (k, m)
+
+
 def test_unaligned_batch(ec):
     k, m, L, B = 8, 2, 4096 + 5, 4
     b = Batch(k, m, L, B, gap=3, offset=1)

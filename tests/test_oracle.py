@@ -202,6 +202,28 @@ def test_oracle_vs_numpy_all_failures(k, m):
             assert (np_ref.recover(np.stack(v), k, m, list(fail)) == strips).all()
 
 
+@pytest.mark.parametrize("m", [1, 2])
+def test_oracle_single_data_strip(m):
+    """k = 1 (the GPU batch API accepts it): every parity strip is a copy of D0
+    and each single / dual failure set rebuilds."""
+    L, B = 1000, 3
+    rng = np.random.default_rng(m)
+    buf = np.zeros((B, 1 + m, L), np.uint8)
+    buf[:, 0] = rng.integers(0, 256, (B, L), dtype=np.uint8)
+    assert oracle.encode_strided(buf.reshape(-1), 1, m, L, B, L, (1 + m) * L) == 0
+    for j in range(1, 1 + m):
+        assert (buf[:, j] == buf[:, 0]).all()
+    good = buf.copy()
+    sets = [(0, 0xFF), (1, 0xFF)] + ([(0, 1), (2, 0), (1, 2)] if m == 2 else [])
+    for f in sets:
+        fail = np.tile(np.array(f, np.uint8), B)
+        for j in f:
+            if j != 0xFF:
+                buf[:, j] = 0x5A
+        assert oracle.recover_strided(buf.reshape(-1), 1, m, L, B, L, (1 + m) * L, fail) == 0
+        assert (buf == good).all(), f
+
+
 def test_splitmix_fixtures(golden):
     from tools.gen_golden import splitmix_stripe
     for c in golden["splitmix_4k"]:
