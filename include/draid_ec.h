@@ -90,7 +90,8 @@ int draid_recover(int k, int m, int len, void **array, int nfail, const int *fai
  * ---------------------------------------------------------------------- */
 
 typedef struct draid_ec_stripe_batch {
-    uint32_t k;            /* data strips per stripe, 1 .. 255                */
+    uint32_t k;            /* data strips per stripe, 1 .. 255 (reconstruct:   
+                            * k + m <= 255)                                    */
     uint32_t m;            /* parity strips: 1 = RAID5 (P), 2 = RAID6 (P, Q)  */
     uint64_t strip_len;    /* bytes per strip (same for every stripe)         */
     uint32_t nstripes;     /* stripes in this batch                           */
