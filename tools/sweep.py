@@ -84,6 +84,26 @@ def make_layout(torch, name, k, m, S, B, dev):
         buf = torch.empty(B * n * ss, dtype=torch.uint8, device=dev)
         idx = torch.arange(B * n, dtype=torch.int64, device=dev)
         table = buf.data_ptr() + idx * ss
+    elif name == "parity_apart":
+        # data strips stripe-major, every stripe's P (Q) in a second region
+        buf = torch.empty(B * n * S, dtype=torch.uint8, device=dev)
+        s = torch.arange(B, dtype=torch.int64, device=dev).repeat_interleave(n)
+        j = torch.arange(n, dtype=torch.int64, device=dev).repeat(B)
+        off = torch.where(j < k, (s * k + j) * S, B * k * S + (s * m + (j - k)) * S)
+        table = buf.data_ptr() + off
+    elif name.startswith("stripe_shuffled"):
+        # stripe-major slots, stripes assigned to slots in a seeded random order
+        # (stripe_shuffled_gG: runs of G consecutive slots stay together)
+        G = int(name.split("_g")[1]) if "_g" in name else 1
+        buf = torch.empty(B * n * S, dtype=torch.uint8, device=dev)
+        g = torch.Generator(device="cpu")
+        g.manual_seed(7)
+        blk = torch.randperm((B + G - 1) // G, generator=g)
+        order = blk.repeat_interleave(G) * G + torch.arange(G).repeat(len(blk))
+        order = order[order < B]
+        slot = order.to(dev).repeat_interleave(n)
+        j = torch.arange(n, dtype=torch.int64, device=dev).repeat(B)
+        table = buf.data_ptr() + (slot * n + j) * S
     elif name == "strip_major":
         buf = torch.empty(n * B * S, dtype=torch.uint8, device=dev)
         s = torch.arange(B, dtype=torch.int64, device=dev).repeat_interleave(n)
