@@ -181,7 +181,10 @@ int draid_ec_ctx_update_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m, uint32_t n
 /* Launch everything queued (non-blocking; blocks only if the descriptor ring
  * is 4 flushes behind).  The context's stream is non-blocking: it does not wait
  * for work on other streams, so every queued buffer must hold its data when
- * flush is called.  draid_ec_ctx_query: 0 idle, 1 running, < 0 error. */
+ * flush is called.  Stripes queued with the same (op, k, m) carry no order
+ * among themselves (the flush may run them in address order); groups run in
+ * the order they were first queued.  draid_ec_ctx_query: 0 idle, 1 running,
+ * < 0 error. */
 int draid_ec_ctx_flush(draid_ec_ctx *ctx);
 int draid_ec_ctx_query(draid_ec_ctx *ctx);
 int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);

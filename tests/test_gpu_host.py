@@ -131,6 +131,7 @@ def test_registered_host_memory(ec):
         # scatter-gather context over the same memory: rebuild two lost strips
         buf[1 * L:2 * L] = 0
         buf[k * L:(k + 1) * L] = 0
+        torch.cuda.synchronize()  # torch's stream before the context's own stream
         ctx = ec.Ctx()
         ctx.reconstruct_sg(k, m, [[(dev + j * L, L)] for j in range(n)], L, [1, k])
         ctx.flush()

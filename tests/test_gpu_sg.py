@@ -73,15 +73,26 @@ def _fill(pool, rng):
 
 @pytest.mark.parametrize("k,m,L,B,prefix", [(4, 1, 4096, 6, False), (8, 2, 8192 + 48, 5, True),
                                             (16, 2, 3000, 3, False), (11, 2, 777, 4, True)])
-def test_sg_encode_and_reconstruct(ec, k, m, L, B, prefix):
+@pytest.mark.parametrize("shuffled", [False, True])
+def test_sg_encode_and_reconstruct(ec, k, m, L, B, prefix, shuffled, monkeypatch):
+    """shuffled: stripes queued out of address order and the context told to
+    reorder every out-of-order group (ec_ctx.cpp address_order; by default only
+    large scattered segments are) -- pointers, lengths and failure pairs must
+    travel together."""
+    if shuffled:
+        monkeypatch.setenv("DRAID_EC_CTX_ADDRESS_ORDER", "2")  # read at ctx creation
     rng = np.random.default_rng(k * L + B)
     pool = Pool(rng, k, m, L, B, prefix=prefix)
     _fill(pool, rng)
     dbuf = torch.from_numpy(pool.host.copy()).to(DEV)
     base = dbuf.data_ptr()
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
     ctx = ec.Ctx()
     try:
-        for s in range(B):
+        order = rng.permutation(B).tolist() if shuffled else list(range(B))
+        if shuffled and order == sorted(order):
+            order = order[::-1]
+        for s in order:
             offs = pool.offsets[s] if prefix else None
             assert ctx.encode_sg(k, m, pool.strips(base, s), L, offs) == 0
         assert ctx.queued() >= B
@@ -106,7 +117,7 @@ def test_sg_encode_and_reconstruct(ec, k, m, L, B, prefix):
                 pool.scatter(erased, s, j, np.full(L, 0x5A, np.uint8))
         dbuf.copy_(torch.from_numpy(erased))
         torch.cuda.synchronize()  # torch's stream before the context's own stream
-        for s in range(B):
+        for s in order:
             offs = pool.offsets[s] if prefix else None
             assert ctx.reconstruct_sg(k, m, pool.strips(base, s), L, fails[s], offs) == 0
         ctx.flush()
@@ -138,23 +149,25 @@ def test_sg_rejects_short_lists(ec):
 
 
 def test_sg_many_stripes_one_flush(ec):
-    """A whole batch of single-iovec stripes in one flush (the SPDK poller shape)."""
+    """A whole batch of single-iovec stripes in one flush (the SPDK poller shape),
+    queued out of address order over 160 MiB: the default context reorders it."""
     k, m, L, B = 8, 2, 65536, 256
     g = torch.Generator(device=DEV)
     g.manual_seed(5)
     buf = torch.randint(0, 256, (B, k + m, L), dtype=torch.uint8, device=DEV, generator=g)
     buf[:, k:] = 0
     base = buf.data_ptr()
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
     ctx = ec.Ctx()
     try:
-        for s in range(B):
+        for s in np.random.default_rng(3).permutation(B).tolist():
             strips = [[(base + (s * (k + m) + j) * L, L)] for j in range(k + m)]
             assert ctx.encode_sg(k, m, strips, L) == 0
         ctx.flush()
         ctx.synchronize()
     finally:
         ctx.close()
-    sample = [0, 101, 255]
+    sample = list(range(0, B, 7)) + [B - 1]
     got = buf[sample].cpu().numpy()
     ref = got.copy()
     assert oracle.encode_strided(ref.reshape(-1), k, m, L, len(sample), L, (k + m) * L) == 0
@@ -179,6 +192,7 @@ def test_sg_uniform_segments(ec, L, piece):
         return [[(base + (s * n + j) * L + o, min(piece, L - o)) for o in range(0, L, piece)]
                 for j in range(n)]
 
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
     ctx = ec.Ctx()
     try:
         for s in range(B):
@@ -225,6 +239,7 @@ def test_sg_adjacent_iovecs_merge(ec):
             o = j * (L + 5 * gap) + a + i * gap
             sc[o:o + ln] = buf[j, a:a + ln]
     bb, sb = buf.data_ptr(), sc.data_ptr()
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
     ctx = ec.Ctx()
     try:
         assert ctx.encode_sg(k, m, [[(bb + j * L + a, ln) for a, ln in pieces]
@@ -262,6 +277,7 @@ def test_sg_single_segment_flush(ec, k, m, L):
     assert oracle.encode_strided(ref.reshape(-1), k, m, L, 3, L, n * L) == 0
     dbuf = torch.from_numpy(host).to(DEV)
     base = dbuf.data_ptr()
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
     ctx = ec.Ctx()
     try:
         # stripe 0 as two segments (a split iovec), then stripes 1 and 2 alone
@@ -283,5 +299,54 @@ def test_sg_single_segment_flush(ec, k, m, L):
         ctx.flush()
         ctx.synchronize()
         assert (dbuf.cpu().numpy() == ref).all()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("order", ["1", "2"])
+def test_sg_shuffled_multi_piece(ec, order, monkeypatch):
+    """More segments than one flush piece (ec_ctx.cpp kPieceBytes), queued in a
+    random order with three different lengths: the reordered pieces, their
+    work lists and failure pairs all line up (order 2: reordered; 1, the
+    default: small segments stay as queued)."""
+    monkeypatch.setenv("DRAID_EC_CTX_ADDRESS_ORDER", order)
+    k, m, C, B = 8, 2, 1024, 12000
+    n = k + m
+    rng = np.random.default_rng(11)
+    host = np.zeros((B, n, C), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (B, k, C), dtype=np.uint8)
+    lens = [C - 16 * (s % 3) for s in range(B)]
+    buf = torch.from_numpy(host).to(DEV)
+    base = buf.data_ptr()
+
+    def strips(s):
+        return [[(base + (s * n + j) * C, lens[s])] for j in range(n)]
+
+    ref = host.copy()
+    for ln in (C, C - 16, C - 32):
+        sel = [s for s in range(B) if lens[s] == ln]
+        sub = np.ascontiguousarray(ref[sel][:, :, :ln])
+        assert oracle.encode_strided(sub.reshape(-1), k, m, ln, len(sel), ln, n * ln) == 0
+        ref[sel, :, :ln] = sub
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
+    ctx = ec.Ctx()
+    try:
+        for s in rng.permutation(B).tolist():
+            assert ctx.encode_sg(k, m, strips(s), lens[s]) == 0
+        ctx.flush()
+        ctx.synchronize()
+        assert (buf.cpu().numpy() == ref).all()
+        fails = [sorted(rng.choice(n, 2, replace=False).tolist()) for _ in range(B)]
+        erased = ref.copy()
+        for s in range(B):
+            for j in fails[s]:
+                erased[s, j, :lens[s]] = 0xA5
+        buf.copy_(torch.from_numpy(erased))
+        torch.cuda.synchronize()  # torch's stream before the context's own stream
+        for s in rng.permutation(B).tolist():
+            assert ctx.reconstruct_sg(k, m, strips(s), lens[s], fails[s]) == 0
+        ctx.flush()
+        ctx.synchronize()
+        assert (buf.cpu().numpy() == ref).all()
     finally:
         ctx.close()

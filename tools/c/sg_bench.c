@@ -3,7 +3,7 @@
  * draid_ec_ctx_encode_sg / _reconstruct_sg / _update_sg, one flush per batch.
  * Reports host walk time per stripe, flush time, and GPU time of the batch
  * (HIP events on the context's stream), for RAID6 8+2 x 64 KiB x 4096 stripes
- * in device memory.  Usage: sg_bench [iov_bytes] [stripes] [reps]
+ * in device memory.  Usage: sg_bench [iov_bytes] [stripes] [reps] [shuffle]
  */
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
@@ -42,6 +42,7 @@ int main(int argc, char **argv)
     const size_t iov_bytes = argc > 1 ? strtoul(argv[1], 0, 0) : S;
     const uint32_t B = argc > 2 ? strtoul(argv[2], 0, 0) : 4096;
     const int reps = argc > 3 ? atoi(argv[3]) : 10;
+    const int shuffle = argc > 4 ? atoi(argv[4]) : 0; /* enqueue stripes in a random order */
     const size_t niov = (S + iov_bytes - 1) / iov_bytes;
     uint8_t *buf = NULL;
     CHECK(draid_ec_device_alloc((void **)&buf, (size_t)B * N * S));
@@ -75,6 +76,18 @@ int main(int argc, char **argv)
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
+    uint32_t *order = malloc(sizeof(uint32_t) * B);
+    for (uint32_t s = 0; s < B; ++s)
+        order[s] = s;
+    if (shuffle) {
+        uint64_t x = 0x9e3779b97f4a7c15ull;
+        for (uint32_t s = B - 1; s > 0; --s) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            const uint32_t r = (uint32_t)(x % (s + 1)), t = order[s];
+            order[s] = order[r];
+            order[r] = t;
+        }
+    }
     int cnt[N];
     for (int j = 0; j < N; ++j)
         cnt[j] = (int)niov;
@@ -85,7 +98,8 @@ int main(int argc, char **argv)
         for (int r = -8; r < reps; ++r) { /* warm-ups fill all 8 descriptor slots */
             CHECK(draid_ec_ctx_synchronize(ctx));
             double t0 = now();
-            for (uint32_t s = 0; s < B; ++s) {
+            for (uint32_t q = 0; q < B; ++q) {
+                const uint32_t s = order[q];
                 const struct iovec *lists[N];
                 for (int j = 0; j < N; ++j)
                     lists[j] = &iov[((size_t)s * N + j) * niov];
@@ -123,10 +137,10 @@ int main(int argc, char **argv)
          * RMW of one chunk: old + new + P + Q read, P + Q written = 6S */
         const double per = op == 0 ? (double)N * S : op == 1 ? (double)(K + 2) * S : 6.0 * S;
         const double user = op == 2 ? (double)S : (double)K * S;
-        printf("{\"op\": \"%s\", \"iov_bytes\": %zu, \"stripes\": %u, \"walk_us_per_stripe\": %.3f, "
+        printf("{\"op\": \"%s\", \"iov_bytes\": %zu, \"stripes\": %u, \"shuffled\": %d, \"walk_us_per_stripe\": %.3f, "
                "\"flush_ms\": %.3f, \"gpu_ms\": %.3f, \"gpu_hbm_gb_s\": %.1f, "
                "\"wall_ms\": %.3f, \"wall_user_gib_s\": %.1f}\n",
-               names[op], iov_bytes, B, walk / reps / B * 1e6, flush / reps * 1e3, gpu / reps,
+               names[op], iov_bytes, B, shuffle, walk / reps / B * 1e6, flush / reps * 1e3, gpu / reps,
                per * B / (gpu / reps * 1e-3) / 1e9, wall / reps * 1e3,
                user * B / (wall / reps) / (1024.0 * 1024 * 1024));
         fflush(stdout);
@@ -134,5 +148,6 @@ int main(int argc, char **argv)
     draid_ec_ctx_destroy(ctx);
     draid_ec_device_free(buf);
     free(iov);
+    free(order);
     return 0;
 }
