@@ -755,6 +755,7 @@ static void run_rebuild(int lvl, int n, uint32_t strip_kb, uint64_t nstripes)
 int main(int argc, char **argv)
 {
     const int cpu_only = argc > 1 && strcmp(argv[1], "--cpu-only") == 0;
+    setvbuf(stdout, NULL, _IOLBF, 0); /* results survive a runtime teardown failure */
     test_geometry();
     test_mapping();
     test_stripe_asm();

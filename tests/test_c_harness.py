@@ -30,3 +30,19 @@ def test_c_harness_gpu(ec):
     out = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "PASS" in out.stdout
+
+
+def test_c_sanitizers():
+    """the host code under sanitizers.  The host RAID layer and
+    stripe cache (compiled from source into the harness) under ASan + UBSan
+    and under TSan (the 8-thread stripe-cache test), and the oracle's round
+    trips under ASan + UBSan -- host paths only, no GPU."""
+    _build()
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "c"), "san"])
+    for name, args in (("test_draid_raid_asan", ["--cpu-only"]),
+                       ("test_draid_raid_tsan", ["--cpu-only"]),
+                       ("test_oracle_san", [])):
+        out = subprocess.run([os.path.join(HERE, "c", name)] + args, capture_output=True,
+                             text=True, timeout=300)
+        assert out.returncode == 0, (name, out.stdout[-2000:], out.stderr[-4000:])
+        assert "PASS" in out.stdout, name

@@ -1,0 +1,20 @@
+# Host code of the library under AddressSanitizer on the MI355X (tests/c/Makefile
+# san-gpu: host side instrumented, kernels not): the C harness end to end, and the
+# scatter-gather context with stripes queued out of order (reordered by default at
+# 64 KiB, and forced with DRAID_EC_CTX_ADDRESS_ORDER=2 at 4 KiB and 1 KiB iovecs).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+# quarantine_size_mb=0: ROCm's ASan runtime otherwise recycles runtime-owned
+# chunks after the HSA runtime has unloaded (a CHECK failure at process exit)
+export ASAN_OPTIONS=detect_leaks=0:quarantine_size_mb=0
+L=gpurun_out/asan.log
+: > $L
+timeout -k 10 300 tests/c/test_draid_raid_asan_gpu >> $L 2>&1 || { tail -40 $L; exit 1; }
+timeout -k 10 120 tests/c/sg_bench_asan_gpu 65536 512 2 1 >> $L 2>&1 || { tail -40 $L; exit 1; }
+DRAID_EC_CTX_ADDRESS_ORDER=2 timeout -k 10 120 tests/c/sg_bench_asan_gpu 4096 256 2 1 >> $L 2>&1 || { tail -40 $L; exit 1; }
+DRAID_EC_CTX_ADDRESS_ORDER=2 timeout -k 10 120 tests/c/sg_bench_asan_gpu 1024 64 2 1 >> $L 2>&1 || { tail -40 $L; exit 1; }
+grep -c "AddressSanitizer" $L && exit 1
+grep -c "^PASS" $L
+tail -12 $L
+echo "asan: clean"
