@@ -350,3 +350,58 @@ def test_sg_shuffled_multi_piece(ec, order, monkeypatch):
         assert (buf.cpu().numpy() == ref).all()
     finally:
         ctx.close()
+
+
+def test_sg_full_size_shuffled(ec):
+    """The headline batch (RAID6 8+2 x 64 KiB x 4096 stripes) through the context,
+    queued in a random order (reordered by the default flush): parity equal to
+    the batched kernel's on the same stripes and sampled stripes equal to the
+    oracle's; then a random dual failure per stripe rebuilt through the context
+    returns the original bytes."""
+    k, m, L, B = 8, 2, 65536, 4096
+    n = k + m
+    g = torch.Generator(device=DEV)
+    g.manual_seed(21)
+    buf = torch.randint(0, 256, (B, n, L), dtype=torch.uint8, device=DEV, generator=g)
+    buf[:, k:] = 0
+    ref = buf.clone()
+    base, rbase = buf.data_ptr(), ref.data_ptr()
+    table = (rbase + torch.arange(B * n, dtype=torch.int64, device=DEV) * L).contiguous()
+    stream = torch.cuda.current_stream().cuda_stream
+    assert ec.encode(ec.make_batch(k, m, L, B, table), stream) == 0
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
+    rng = np.random.default_rng(8)
+
+    def strips(s):
+        return [[(base + (s * n + j) * L, L)] for j in range(n)]
+
+    ctx = ec.Ctx()
+    try:
+        for s in rng.permutation(B).tolist():
+            assert ctx.encode_sg(k, m, strips(s), L) == 0
+        ctx.flush()
+        ctx.synchronize()
+        assert torch.equal(buf, ref)
+        sample = [0, 1234, B - 1]
+        got = buf[sample].cpu().numpy()
+        assert (got == oracle_encode_np(got, k, m)).all()
+        fails = [sorted(rng.choice(n, 2, replace=False).tolist()) for _ in range(B)]
+        f = torch.tensor(fails, dtype=torch.int64, device=DEV)
+        si = torch.arange(B, device=DEV)
+        buf[si, f[:, 0]] = 0x6B
+        buf[si, f[:, 1]] = 0xB6
+        torch.cuda.synchronize()
+        for s in rng.permutation(B).tolist():
+            assert ctx.reconstruct_sg(k, m, strips(s), L, fails[s]) == 0
+        ctx.flush()
+        ctx.synchronize()
+        assert torch.equal(buf, ref)
+    finally:
+        ctx.close()
+
+
+def oracle_encode_np(stripes, k, m):
+    out = np.ascontiguousarray(stripes.copy())
+    B, n, L = out.shape
+    assert oracle.encode_strided(out.reshape(-1), k, m, L, B, L, n * L) == 0
+    return out

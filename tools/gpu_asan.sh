@@ -2,6 +2,7 @@
 # san-gpu: host side instrumented, kernels not): the C harness end to end, and the
 # scatter-gather context with stripes queued out of order (reordered by default at
 # 64 KiB, and forced with DRAID_EC_CTX_ADDRESS_ORDER=2 at 4 KiB and 1 KiB iovecs).
+# Build first, here: make -C tests/c san-gpu (the binaries are not kept in the tree).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
