@@ -333,12 +333,16 @@ int draid_ec_set_device(int device)
 
 int draid_ec_device_count(int* count)
 {
+    if (!count)
+        return fail_arg("device_count: count is NULL");
     hipError_t e = hipGetDeviceCount(count);
     return e == hipSuccess ? 0 : fail_hip(e, "hipGetDeviceCount");
 }
 
 int draid_ec_stream_create(void** stream)
 {
+    if (!stream)
+        return fail_arg("stream_create: stream is NULL");
     hipStream_t s = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e != hipSuccess)
@@ -371,6 +375,8 @@ int draid_ec_stream_synchronize(void* stream)
 
 int draid_ec_device_alloc(void** ptr, size_t bytes)
 {
+    if (!ptr)
+        return fail_arg("device_alloc: ptr is NULL");
     hipError_t e = hipMalloc(ptr, bytes);
     return e == hipSuccess ? 0 : fail_hip(e, "hipMalloc");
 }

@@ -100,3 +100,8 @@ def test_argument_errors_before_any_launch():
     assert L.draid_xor_gen(2, 64, arr) == 1           # fewer than 2 sources + dest
     assert L.draid_pq_gen(4, 48, arr) == 1            # len % 32 != 0
     assert L.draid_gf_vect_mul(31, bytes(32), dummy, dummy) == 1
+    # NULL out-pointers of the runtime helpers
+    assert L.draid_ec_device_count(None) == 1
+    assert L.draid_ec_stream_create(None) == 1
+    assert L.draid_ec_device_alloc(None, C.c_size_t(64)) == 1
+    assert L.draid_ec_host_device_pointer(dummy, None) == 1
