@@ -67,6 +67,7 @@ struct draid_ec_ctx {
     int address_order = 1;  // DRAID_EC_CTX_ADDRESS_ORDER: 0 off, 1 auto, 2 any out-of-order group
                             // (diagnostics and tests)
     std::vector<uint32_t> perm, bucket;
+    uint64_t autoflush = 0;  // launch a group once it holds this many segments (0 = off)
 };
 
 namespace {
@@ -155,6 +156,8 @@ bool iter_seek(IovIter& it, size_t offset)
     return true;
 }
 
+int flush_group(draid_ec_ctx* c, Group& g);
+
 // The walk of raid5_xor_stripe: runs of n = min over strips of the bytes left
 // in each strip's current iovec; one descriptor per run.
 int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* const* iovs,
@@ -222,6 +225,12 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
         g.fail.insert(g.fail.end(), meta, meta + nmeta);
         ++c->queued_segments;
         remaining -= run;
+    }
+    if (c->autoflush && g.len.size() >= c->autoflush) {
+        const size_t nseg = g.len.size();
+        const int rc = flush_group(c, g);
+        c->queued_segments -= nseg;
+        return rc;
     }
     return 0;
 }
@@ -541,5 +550,13 @@ int draid_ec_ctx_synchronize(draid_ec_ctx* c)
 }
 
 uint64_t draid_ec_ctx_queued(draid_ec_ctx* c) { return c ? c->queued_segments : 0; }
+
+int draid_ec_ctx_set_autoflush(draid_ec_ctx* c, uint64_t segments)
+{
+    if (!c)
+        return ctx_arg("ctx is NULL");
+    c->autoflush = segments;
+    return 0;
+}
 
 }  // extern "C"

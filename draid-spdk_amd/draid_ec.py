@@ -34,7 +34,7 @@ EXPORTS = (
     "draid_ec_ctx_flush", "draid_ec_ctx_query", "draid_ec_ctx_synchronize",
     "draid_ec_ctx_queued", "draid_ec_host_encode", "draid_ec_host_reconstruct",
     "draid_ec_encode_strided", "draid_ec_reconstruct_strided",
-    "draid_ec_ctx_update_sg", "draid_ec_host_device_pointer",
+    "draid_ec_ctx_update_sg", "draid_ec_host_device_pointer", "draid_ec_ctx_set_autoflush",
 )
 
 
@@ -114,6 +114,7 @@ def lib() -> C.CDLL:
         L.draid_ec_ctx_stream.restype = vp
         L.draid_ec_ctx_queued.argtypes = [vp]
         L.draid_ec_ctx_queued.restype = C.c_uint64
+        L.draid_ec_ctx_set_autoflush.argtypes = [vp, C.c_uint64]
         L.draid_ec_ctx_encode_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t]
         L.draid_ec_ctx_reconstruct_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp,
                                                   C.c_size_t, i32, vp]
@@ -330,6 +331,9 @@ class Ctx:
 
     def queued(self):
         return lib().draid_ec_ctx_queued(self.h)
+
+    def set_autoflush(self, segments: int):
+        return _check(lib().draid_ec_ctx_set_autoflush(self.h, segments), "ctx_set_autoflush")
 
 
 def set_variant(v: int) -> None:

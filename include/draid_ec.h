@@ -90,7 +90,7 @@ int draid_recover(int k, int m, int len, void **array, int nfail, const int *fai
  * ---------------------------------------------------------------------- */
 
 typedef struct draid_ec_stripe_batch {
-    uint32_t k;            /* data strips per stripe, 1 .. 255 (reconstruct:   
+    uint32_t k;            /* data strips per stripe, 1 .. 255 (reconstruct:
                             * k + m <= 255)                                    */
     uint32_t m;            /* parity strips: 1 = RAID5 (P), 2 = RAID6 (P, Q)  */
     uint64_t strip_len;    /* bytes per strip (same for every stripe)         */
@@ -189,6 +189,14 @@ int draid_ec_ctx_flush(draid_ec_ctx *ctx);
 int draid_ec_ctx_query(draid_ec_ctx *ctx);
 int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);
 uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last flush */
+
+/* Launch an (op, k, m) group as soon as it holds `segments` queued segments,
+ * from inside the queueing call (0 = only at draid_ec_ctx_flush, the default).
+ * For callers whose buffers hold their data when a stripe is queued (an SPDK
+ * module queues a stripe once its data or prereads are in): the GPU then runs
+ * while the host walks the rest of the batch.  A queueing call that launches
+ * returns the launch's error, if any. */
+int draid_ec_ctx_set_autoflush(draid_ec_ctx *ctx, uint64_t segments);
 
 /* ------------------------------------------------------------------------
  * 2c. Host-resident stripes (PCIe-inclusive path)

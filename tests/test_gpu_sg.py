@@ -405,3 +405,45 @@ def oracle_encode_np(stripes, k, m):
     B, n, L = out.shape
     assert oracle.encode_strided(out.reshape(-1), k, m, L, B, L, n * L) == 0
     return out
+
+
+def test_sg_autoflush(ec):
+    """draid_ec_ctx_set_autoflush: groups launch from inside the queueing calls
+    once they hold N segments (encode and reconstruct groups alike); the final
+    flush launches the rest, and the results equal the oracle's."""
+    k, m, L, B, N = 8, 2, 16384, 300, 64
+    n = k + m
+    g = torch.Generator(device=DEV)
+    g.manual_seed(9)
+    buf = torch.randint(0, 256, (B, n, L), dtype=torch.uint8, device=DEV, generator=g)
+    buf[:, k:] = 0
+    base = buf.data_ptr()
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
+    rng = np.random.default_rng(4)
+
+    def strips(s):
+        return [[(base + (s * n + j) * L, L)] for j in range(n)]
+
+    ctx = ec.Ctx()
+    try:
+        ctx.set_autoflush(N)
+        for i, s in enumerate(rng.permutation(B).tolist()):
+            assert ctx.encode_sg(k, m, strips(s), L) == 0
+            assert ctx.queued() == (i + 1) % N
+        ctx.flush()
+        ctx.synchronize()
+        got = buf.cpu().numpy()
+        assert (got == oracle_encode_np(got, k, m)).all()
+        fails = [sorted(rng.choice(n, 2, replace=False).tolist()) for _ in range(B)]
+        erased = got.copy()
+        for s in range(B):
+            erased[s, fails[s]] = 0x99
+        buf.copy_(torch.from_numpy(erased))
+        torch.cuda.synchronize()
+        for s in rng.permutation(B).tolist():
+            assert ctx.reconstruct_sg(k, m, strips(s), L, fails[s]) == 0
+        ctx.flush()
+        ctx.synchronize()
+        assert (buf.cpu().numpy() == got).all()
+    finally:
+        ctx.close()

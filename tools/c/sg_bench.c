@@ -3,7 +3,7 @@
  * draid_ec_ctx_encode_sg / _reconstruct_sg / _update_sg, one flush per batch.
  * Reports host walk time per stripe, flush time, and GPU time of the batch
  * (HIP events on the context's stream), for RAID6 8+2 x 64 KiB x 4096 stripes
- * in device memory.  Usage: sg_bench [iov_bytes] [stripes] [reps] [shuffle]
+ * in device memory.  Usage: sg_bench [iov_bytes] [stripes] [reps] [shuffle] [autoflush]
  */
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
@@ -43,6 +43,7 @@ int main(int argc, char **argv)
     const uint32_t B = argc > 2 ? strtoul(argv[2], 0, 0) : 4096;
     const int reps = argc > 3 ? atoi(argv[3]) : 10;
     const int shuffle = argc > 4 ? atoi(argv[4]) : 0; /* enqueue stripes in a random order */
+    const uint64_t autoflush = argc > 5 ? strtoull(argv[5], 0, 0) : 0; /* ctx autoflush segments */
     const size_t niov = (S + iov_bytes - 1) / iov_bytes;
     uint8_t *buf = NULL;
     CHECK(draid_ec_device_alloc((void **)&buf, (size_t)B * N * S));
@@ -72,6 +73,7 @@ int main(int argc, char **argv)
             }
     draid_ec_ctx *ctx;
     CHECK(draid_ec_ctx_create(&ctx));
+    CHECK(draid_ec_ctx_set_autoflush(ctx, autoflush));
     hipStream_t st = (hipStream_t)draid_ec_ctx_stream(ctx);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
@@ -137,10 +139,10 @@ int main(int argc, char **argv)
          * RMW of one chunk: old + new + P + Q read, P + Q written = 6S */
         const double per = op == 0 ? (double)N * S : op == 1 ? (double)(K + 2) * S : 6.0 * S;
         const double user = op == 2 ? (double)S : (double)K * S;
-        printf("{\"op\": \"%s\", \"iov_bytes\": %zu, \"stripes\": %u, \"shuffled\": %d, \"walk_us_per_stripe\": %.3f, "
+        printf("{\"op\": \"%s\", \"iov_bytes\": %zu, \"stripes\": %u, \"shuffled\": %d, \"autoflush\": %llu, \"walk_us_per_stripe\": %.3f, "
                "\"flush_ms\": %.3f, \"gpu_ms\": %.3f, \"gpu_hbm_gb_s\": %.1f, "
                "\"wall_ms\": %.3f, \"wall_user_gib_s\": %.1f}\n",
-               names[op], iov_bytes, B, shuffle, walk / reps / B * 1e6, flush / reps * 1e3, gpu / reps,
+               names[op], iov_bytes, B, shuffle, (unsigned long long)autoflush, walk / reps / B * 1e6, flush / reps * 1e3, gpu / reps,
                per * B / (gpu / reps * 1e-3) / 1e9, wall / reps * 1e3,
                user * B / (wall / reps) / (1024.0 * 1024 * 1024));
         fflush(stdout);
