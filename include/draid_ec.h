@@ -195,7 +195,10 @@ uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last
  * For callers whose buffers hold their data when a stripe is queued (an SPDK
  * module queues a stripe once its data or prereads are in): the GPU then runs
  * while the host walks the rest of the batch.  A queueing call that launches
- * returns the launch's error, if any. */
+ * returns the launch's error, if any.  Such a launch carries only its own
+ * group: it may run before segments queued earlier in other groups, so work
+ * on the same buffers in different groups needs a flush in between (as it
+ * does anyway when a later group must run first). */
 int draid_ec_ctx_set_autoflush(draid_ec_ctx *ctx, uint64_t segments);
 
 /* ------------------------------------------------------------------------
