@@ -279,6 +279,11 @@ def main() -> None:
         torch.cuda.synchronize(dev)
         verified = bool(torch.equal(view[:, :k], good))
         del good
+        if world > 1:  # every rank's shard must come back
+            vt = torch.tensor([1.0 if verified else 0.0], dtype=torch.float64,
+                              device=dev if args.dist_backend == "nccl" else torch.device("cpu"))
+            dist.all_reduce(vt, op=dist.ReduceOp.MIN)
+            verified = bool(vt.item() == 1.0)
 
     value = units / elapsed / GIB
     workload = args.config
