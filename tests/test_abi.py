@@ -105,3 +105,4 @@ def test_argument_errors_before_any_launch():
     assert L.draid_ec_stream_create(None) == 1
     assert L.draid_ec_device_alloc(None, C.c_size_t(64)) == 1
     assert L.draid_ec_host_device_pointer(dummy, None) == 1
+    assert L.draid_ec_ctx_set_autoflush(None, C.c_uint64(1024)) == 1
