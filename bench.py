@@ -259,8 +259,9 @@ def main() -> None:
     t1 = time.perf_counter()
 
     elapsed = t1 - t0
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    rec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    enc_all = [e[0].elapsed_time(e[1]) for e in ev]
+    rec_all = [e[1].elapsed_time(e[2]) for e in ev]
+    enc_ms, rec_ms = float(np.mean(enc_all)), float(np.mean(rec_all))
     units = 2.0 * k * S * B * args.steps  # user-data bytes through both passes
     elapsed, units = reduce_timing(elapsed, units,
                                    dev if args.dist_backend == "nccl" else torch.device("cpu"))
@@ -334,6 +335,8 @@ def main() -> None:
         "breakdown": {
             "encode_ms": round(enc_ms, 4),
             "reconstruct_ms": round(rec_ms, 4),
+            "encode_ms_median": round(float(np.median(enc_all)), 4),
+            "reconstruct_ms_median": round(float(np.median(rec_all)), 4),
             "encode_user_gib_s": round(k * S * B / (enc_ms * 1e-3) / GIB, 1),
             "reconstruct_user_gib_s": round(k * S * B / (rec_ms * 1e-3) / GIB, 1),
             "encode_hbm_gb_s": round(enc_gbs, 1),
