@@ -159,7 +159,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="raid6_8p2_64k", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=None,
                     help="stripes per GPU (override); with --strong, the whole job's")
