@@ -200,8 +200,11 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             // any following iovecs that continue it in memory (a split buffer
             // needs no extra descriptors; the arithmetic is per byte, so merging
             // adjacent runs cannot change the result).
-            size_t avail = t.v[t.idx].iov_len - t.off;
-            const uint8_t* end = static_cast<const uint8_t*>(t.v[t.idx].iov_base) + t.v[t.idx].iov_len;
+            const struct iovec& cur = t.v[t.idx];
+            size_t avail = cur.iov_len - t.off;
+            if (avail >= run)
+                continue;  // this strip does not shorten the run
+            const uint8_t* end = static_cast<const uint8_t*>(cur.iov_base) + cur.iov_len;
             for (int x = t.idx + 1; x < t.cnt && avail < run; ++x) {
                 if (t.v[x].iov_len == 0)
                     continue;
@@ -212,9 +215,12 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             }
             run = std::min<size_t>(run, avail);
         }
+        const size_t at = g.ptrs.size();
+        g.ptrs.resize(at + n);
+        const void** out = g.ptrs.data() + at;
         for (uint32_t j = 0; j < n; ++j) {
             IovIter& t = it[j];
-            g.ptrs.push_back(static_cast<const uint8_t*>(t.v[t.idx].iov_base) + t.off);
+            out[j] = static_cast<const uint8_t*>(t.v[t.idx].iov_base) + t.off;
             t.off += run;
             while (t.idx < t.cnt && t.off > t.v[t.idx].iov_len) {  // crossed merged iovecs
                 t.off -= t.v[t.idx].iov_len;
@@ -222,7 +228,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             }
         }
         g.len.push_back(static_cast<uint32_t>(run));
-        g.fail.insert(g.fail.end(), meta, meta + nmeta);
+        if (nmeta)
+            g.fail.insert(g.fail.end(), meta, meta + nmeta);
         ++c->queued_segments;
         remaining -= run;
     }
