@@ -20,6 +20,7 @@
 #include <sys/uio.h>
 
 #include <algorithm>
+#include <deque>
 #include <vector>
 
 #include "../../include/draid_ec.h"
@@ -32,12 +33,80 @@ constexpr size_t kPieceBytes = 1u << 20;       // descriptors per launch (≈ 1 
 constexpr size_t kMinPieceSegments = 4096;
 constexpr uint64_t kMaxSegment = 1ull << 30;
 
+// Growable array in pinned host memory.  The walk writes a group's strip
+// pointers here and the flush DMAs them to the device straight from it, so the
+// pointers -- (k+m) * 8 bytes of every run, nearly all of a piece's
+// descriptor bytes -- are written once, not walked into pageable memory and
+// then packed into a ring slot.  Growth never initialises the new elements.
+class PinnedPtrs {
+public:
+    PinnedPtrs() = default;
+    PinnedPtrs(const PinnedPtrs&) = delete;
+    PinnedPtrs& operator=(const PinnedPtrs&) = delete;
+    ~PinnedPtrs() { if (p_) (void)hipHostFree(p_); }
+    void swap(PinnedPtrs& o) { std::swap(p_, o.p_); std::swap(n_, o.n_); std::swap(cap_, o.cap_); }
+    size_t size() const { return n_; }
+    const void** data() { return p_; }
+    const void* operator[](size_t i) const { return p_[i]; }
+    void clear() { n_ = 0; }
+    void shrink(size_t n) { n_ = std::min(n_, n); }
+    // Appends `add` uninitialised elements; null when pinned memory runs out.
+    const void** grow(size_t add)
+    {
+        if (n_ + add > cap_) {
+            size_t cap = std::max<size_t>(cap_ ? cap_ * 2 : (1u << 20) / sizeof(void*), n_ + add);
+            void* q = nullptr;
+            if (hipHostMalloc(&q, cap * sizeof(void*), hipHostMallocDefault) != hipSuccess)
+                return nullptr;
+            if (n_)
+                memcpy(q, p_, n_ * sizeof(void*));
+            if (p_)
+                (void)hipHostFree(p_);  // never in flight: see Group::ready()
+            p_ = static_cast<const void**>(q);
+            cap_ = cap;
+        }
+        const void** out = p_ + n_;
+        n_ += add;
+        return out;
+    }
+
+private:
+    const void** p_ = nullptr;
+    size_t n_ = 0, cap_ = 0;
+};
+
 struct Group {
+    Group(int op_, uint32_t k_, uint32_t m_) : op(op_), k(k_), m(m_) {}
+    Group(const Group&) = delete;
+    Group& operator=(const Group&) = delete;
+    ~Group()
+    {
+        for (hipEvent_t e : uploaded)
+            if (e)
+                (void)hipEventDestroy(e);
+    }
     int op;  // 0 encode, 1 reconstruct, 2 read-modify-write update
     uint32_t k, m;                  // op 2: k = 2 * touched chunks (old/new list pairs)
-    std::vector<const void*> ptrs;  // [nseg][k+m]
+    PinnedPtrs ptrs;                // [nseg][k+m]
     std::vector<uint32_t> len;      // [nseg]
     std::vector<uint8_t> fail;      // [nseg][2] failure pair (op 1) / [nseg][k/2] exponents (op 2)
+    // Double-buffered pointer storage: a flush whose pieces DMA straight from
+    // `ptrs` records uploaded[0] behind those copies and swaps in `spare`, so the
+    // next batch is walked while the copies run; a buffer is written again only
+    // once its copies are done.
+    PinnedPtrs spare;
+    hipEvent_t uploaded[2] = {nullptr, nullptr};  // [0] for ptrs, [1] for spare
+    bool pending[2] = {false, false};
+    bool direct = false;  // this flush DMA'd from ptrs
+
+    int ready()  // before writing into ptrs
+    {
+        if (!pending[0])
+            return 0;
+        pending[0] = false;
+        const hipError_t e = hipEventSynchronize(uploaded[0]);
+        return e == hipSuccess ? 0 : draid::fail_hip(e, "hipEventSynchronize(descriptors)");
+    }
 };
 
 struct Slot {
@@ -60,7 +129,7 @@ struct draid_ec_ctx {
     hipStream_t stream = nullptr;   // kernels
     hipStream_t copy = nullptr;     // descriptor uploads
     int device = 0;
-    std::vector<Group> groups;
+    std::deque<Group> groups;  // deque: groups never move (pinned storage, events)
     Slot slots[kSlots];
     int next = 0;
     uint64_t queued_segments = 0;
@@ -129,7 +198,7 @@ Group& group_for(draid_ec_ctx* c, int op, uint32_t k, uint32_t m)
     for (Group& g : c->groups)
         if (g.op == op && g.k == k && g.m == m)
             return g;
-    c->groups.push_back(Group{op, k, m, {}, {}, {}});
+    c->groups.emplace_back(op, k, m);
     return c->groups.back();
 }
 
@@ -176,10 +245,12 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             return ctx_arg("iovec list shorter than offset");
     }
     Group& g = group_for(c, op, k, m);
+    if (const int rc = g.ready())
+        return rc;
     const size_t n_ptrs = g.ptrs.size(), n_len = g.len.size(), n_fail = g.fail.size();
     const uint64_t n_q = c->queued_segments;
     auto rollback = [&](const char* what) {  // a rejected stripe queues nothing
-        g.ptrs.resize(n_ptrs);
+        g.ptrs.shrink(n_ptrs);
         g.len.resize(n_len);
         g.fail.resize(n_fail);
         c->queued_segments = n_q;
@@ -215,9 +286,9 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             }
             run = std::min<size_t>(run, avail);
         }
-        const size_t at = g.ptrs.size();
-        g.ptrs.resize(at + n);
-        const void** out = g.ptrs.data() + at;
+        const void** out = g.ptrs.grow(n);
+        if (!out)
+            return rollback("out of pinned host memory for descriptors");
         for (uint32_t j = 0; j < n; ++j) {
             IovIter& t = it[j];
             out[j] = static_cast<const uint8_t*>(t.v[t.idx].iov_base) + t.off;
@@ -247,7 +318,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
 // stream once the copy has landed.  Copies therefore overlap the kernels of
 // earlier pieces and flushes.
 // `perm` (may be null): segment i of the group is g's segment perm[i].
-int flush_piece(draid_ec_ctx* c, const Group& g, const uint32_t* perm, size_t s0, size_t s1)
+int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size_t s1)
 {
     const size_t nseg = s1 - s0;
     const uint32_t n = g.k + g.m;
@@ -316,20 +387,30 @@ int flush_piece(draid_ec_ctx* c, const Group& g, const uint32_t* perm, size_t s0
             memcpy(hp + i * n, g.ptrs.data() + (size_t)perm[s0 + i] * n, n * sizeof(void*));
         for (size_t i = 0; nmeta && i < nseg; ++i)
             memcpy(h + o_fail + i * nmeta, g.fail.data() + (size_t)perm[s0 + i] * nmeta, nmeta);
-    } else {
-        memcpy(h + o_ptr, g.ptrs.data() + s0 * n, nseg * n * sizeof(void*));
-        if (nmeta)
-            memcpy(h + o_fail, g.fail.data() + s0 * nmeta, nseg * nmeta);
+    } else if (nmeta) {
+        memcpy(h + o_fail, g.fail.data() + s0 * nmeta, nseg * nmeta);
     }
     if (!uniform)
         memcpy(h + o_len, lenp, nseg * sizeof(uint32_t));
     if (!work.empty())
         memcpy(h + o_work, work.data(), work.size() * sizeof(uint32_t));
-    // One DMA of the piece's descriptors.  (Reading them in place from the pinned
-    // slot instead was measured slower: 1.39 vs 1.00 ms for 4096 stripes of 4 KiB
-    // iovecs -- the per-item pointer loads then pay PCIe latency.)
-    if ((e = hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, c->copy)) !=
-        hipSuccess)
+    // DMA the piece's descriptors: in address order the pointer table comes
+    // straight from the group's pinned storage, the rest (lengths, failure
+    // pairs, work list; none for uniform encode segments) from the slot.
+    // (Reading them in place from pinned memory instead was measured slower:
+    // 1.39 vs 1.00 ms for 4096 stripes of 4 KiB iovecs -- the per-item pointer
+    // loads then pay PCIe latency.)
+    if (perm)
+        e = hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, c->copy);
+    else {
+        e = hipMemcpyAsync(static_cast<uint8_t*>(sl.dev) + o_ptr, g.ptrs.data() + s0 * n,
+                           nseg * n * sizeof(void*), hipMemcpyHostToDevice, c->copy);
+        if (e == hipSuccess && bytes > o_len)
+            e = hipMemcpyAsync(static_cast<uint8_t*>(sl.dev) + o_len, h + o_len, bytes - o_len,
+                               hipMemcpyHostToDevice, c->copy);
+        g.direct = true;
+    }
+    if (e != hipSuccess)
         return ctx_fail(e, "hipMemcpyAsync(descriptors)");
     if ((e = hipEventRecord(sl.uploaded, c->copy)) != hipSuccess ||
         (e = hipStreamWaitEvent(c->stream, sl.uploaded, 0)) != hipSuccess)
@@ -390,8 +471,26 @@ int flush_group(draid_ec_ctx* c, Group& g)
     const size_t piece = std::max<size_t>(kMinPieceSegments, kPieceBytes / per_seg);
     const uint32_t* perm = address_order(c, g);
     int rc = 0;
+    g.direct = false;
     for (size_t s0 = 0; s0 < nseg && rc == 0; s0 += piece)
         rc = flush_piece(c, g, perm, s0, std::min(nseg, s0 + piece));
+    if (g.direct) {  // copies from g.ptrs in flight: walk the next batch into the spare
+        hipError_t e = hipSuccess;
+        if (!g.uploaded[0])
+            e = hipEventCreateWithFlags(&g.uploaded[0], hipEventDisableTiming);
+        if (e == hipSuccess)
+            e = hipEventRecord(g.uploaded[0], c->copy);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(c->copy);
+            if (rc == 0)
+                rc = ctx_fail(e, "descriptor storage event");
+        } else {
+            g.pending[0] = true;
+        }
+        g.ptrs.swap(g.spare);
+        std::swap(g.uploaded[0], g.uploaded[1]);
+        std::swap(g.pending[0], g.pending[1]);
+    }
     g.ptrs.clear();
     g.len.clear();
     g.fail.clear();
