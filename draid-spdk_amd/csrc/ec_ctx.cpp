@@ -202,26 +202,37 @@ Group& group_for(draid_ec_ctx* c, int op, uint32_t k, uint32_t m)
     return c->groups.back();
 }
 
-// Iterator over one strip's iovec list (raid5_simple.c iov_iter).
+// Iterator over one strip's iovec list (raid5_simple.c iov_iter).  It carries
+// the current position and the bytes left in the current iovec, so the walk
+// reads the iovec array only when an iovec ends.
 struct IovIter {
     const struct iovec* v;
     int cnt;
     int idx;
-    size_t off;
+    const uint8_t* p;  // current byte
+    size_t left;       // bytes left in v[idx] from p
+
+    void enter(int i)
+    {
+        idx = i;
+        p = static_cast<const uint8_t*>(v[i].iov_base);
+        left = v[i].iov_len;
+    }
 };
 
 // Positions the iterator `offset` bytes into the list (raid5.c:235-255).
 bool iter_seek(IovIter& it, size_t offset)
 {
-    it.idx = 0;
-    it.off = 0;
-    while (it.idx < it.cnt && offset >= it.v[it.idx].iov_len) {
-        offset -= it.v[it.idx].iov_len;
-        ++it.idx;
+    int i = 0;
+    while (i < it.cnt && offset >= it.v[i].iov_len) {
+        offset -= it.v[i].iov_len;
+        ++i;
     }
-    if (it.idx >= it.cnt)
+    if (i >= it.cnt)
         return false;
-    it.off = offset;
+    it.enter(i);
+    it.p += offset;
+    it.left -= offset;
     return true;
 }
 
@@ -240,7 +251,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     for (uint32_t j = 0; j < n; ++j) {
         if (!iovs || !iovs[j] || !iovcnt || iovcnt[j] < 0)
             return ctx_arg("iovec list missing");
-        it[j] = IovIter{iovs[j], iovcnt[j], 0, 0};
+        it[j] = IovIter{iovs[j], iovcnt[j], 0, nullptr, 0};
         if (len && !iter_seek(it[j], offset ? offset[j] : 0))
             return ctx_arg("iovec list shorter than offset");
     }
@@ -261,21 +272,19 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
         size_t run = std::min<size_t>(remaining, kMaxSegment);
         for (uint32_t j = 0; j < n; ++j) {
             IovIter& t = it[j];
-            while (t.idx < t.cnt && t.off == t.v[t.idx].iov_len) {
-                ++t.idx;  // skip exhausted / zero-length entries
-                t.off = 0;
+            if (t.left >= run)
+                continue;  // this strip does not shorten the run
+            while (t.left == 0) {  // skip exhausted / zero-length entries
+                if (t.idx + 1 >= t.cnt)
+                    return rollback("iovec list shorter than len");
+                t.enter(t.idx + 1);
             }
-            if (t.idx >= t.cnt)
-                return rollback("iovec list shorter than len");
             // Bytes available contiguously from here: the rest of this iovec plus
             // any following iovecs that continue it in memory (a split buffer
             // needs no extra descriptors; the arithmetic is per byte, so merging
             // adjacent runs cannot change the result).
-            const struct iovec& cur = t.v[t.idx];
-            size_t avail = cur.iov_len - t.off;
-            if (avail >= run)
-                continue;  // this strip does not shorten the run
-            const uint8_t* end = static_cast<const uint8_t*>(cur.iov_base) + cur.iov_len;
+            size_t avail = t.left;
+            const uint8_t* end = t.p + t.left;
             for (int x = t.idx + 1; x < t.cnt && avail < run; ++x) {
                 if (t.v[x].iov_len == 0)
                     continue;
@@ -291,12 +300,19 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             return rollback("out of pinned host memory for descriptors");
         for (uint32_t j = 0; j < n; ++j) {
             IovIter& t = it[j];
-            out[j] = static_cast<const uint8_t*>(t.v[t.idx].iov_base) + t.off;
-            t.off += run;
-            while (t.idx < t.cnt && t.off > t.v[t.idx].iov_len) {  // crossed merged iovecs
-                t.off -= t.v[t.idx].iov_len;
-                ++t.idx;
+            out[j] = t.p;
+            if (run <= t.left) {
+                t.p += run;
+                t.left -= run;
+                continue;
             }
+            size_t r = run;  // crossed merged iovecs
+            while (r > t.left) {
+                r -= t.left;
+                t.enter(t.idx + 1);
+            }
+            t.p += r;
+            t.left -= r;
         }
         g.len.push_back(static_cast<uint32_t>(run));
         if (nmeta)

@@ -2,13 +2,13 @@
 # group's pinned storage (current library) against packing them into a ring
 # slot first (the previous ec_ctx.cpp, built beside it into
 # draid-spdk_amd/ab_old/ and selected through LD_LIBRARY_PATH, which takes
-# precedence over sg_bench's RUNPATH).  sg tests on the current library first.
-# The old library was built here from `git show 04e7618:draid-spdk_amd/csrc/ec_ctx.cpp`
+# precedence over sg_bench's RUNPATH).  GPU tests on the current library first.
+# The old library was built here from `git show <previous commit>:draid-spdk_amd/csrc/ec_ctx.cpp`
 # with the Makefile's HIPFLAGS, linked against the other build/*.o objects.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_sg.py tests/test_gpu_threads.py tests/test_gpu_host.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/pytest_sg.log 2>&1 || { tail -30 gpurun_out/pytest_sg.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/pytest_sg.log 2>&1 || { tail -30 gpurun_out/pytest_sg.log; exit 1; }
 tail -1 gpurun_out/pytest_sg.log
 out=gpurun_out/sg_direct_ab.jsonl
 rm -f $out
