@@ -143,8 +143,9 @@ int draid_ec_reconstruct_strided(const draid_ec_strided_stripes *s, const uint8_
  * The reference walks each chunk's iovec list and calls isa-l once per
  * contiguous run (raid5_xor_iovs, raid5.c:221-283; raid5_xor_stripe,
  * raid5_simple.c:141-203).  A context runs the same walk on the host but queues
- * each run as a gather descriptor; draid_ec_ctx_flush() uploads all queued
- * descriptors with one DMA and launches one kernel per (op, k, m) group.
+ * each run as a gather descriptor; draid_ec_ctx_flush() uploads the queued
+ * descriptors in ~1 MiB pieces (copy stream) and launches one kernel per piece
+ * of each (op, k, m) group, so uploads overlap earlier kernels.
  * A context owns a stream and is used by one thread (one per SPDK io_channel).
  * ---------------------------------------------------------------------- */
 
