@@ -279,6 +279,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                     return rollback("iovec list shorter than len");
                 t.enter(t.idx + 1);
             }
+            if (t.left >= run)
+                continue;  // the next iovec covers the run: no merge scan
             // Bytes available contiguously from here: the rest of this iovec plus
             // any following iovecs that continue it in memory (a split buffer
             // needs no extra descriptors; the arithmetic is per byte, so merging
