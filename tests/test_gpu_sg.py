@@ -447,3 +447,43 @@ def test_sg_autoflush(ec):
         assert (buf.cpu().numpy() == got).all()
     finally:
         ctx.close()
+
+
+def test_sg_back_to_back_flushes(ec):
+    """Flushes issued back to back with no synchronisation between them, the
+    next batch walked while the previous one's pointer tables are still being
+    copied from the context's pinned storage (ec_ctx.cpp Group: double-buffered,
+    a buffer is written again only after its copies are done).  Batch sizes make
+    the storage grow (one batch of 2100 stripes x 16 runs x 10 strips is past its
+    first 1 MiB) between small ones; every stripe must equal the oracle's."""
+    k, m, L, piece = 8, 2, 8192, 512
+    n = k + m
+    batches = [50, 1500, 30, 2100, 7]
+    B = sum(batches)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(21)
+    buf = torch.randint(0, 256, (B, n, L), dtype=torch.uint8, device=DEV, generator=g)
+    buf[:, k:] = 0
+    base = buf.data_ptr()
+    torch.cuda.synchronize()  # torch's stream before the context's own stream
+
+    def strips(s):  # pieces listed in reverse address order: nothing merges
+        return [[(base + (s * n + j) * L + o, piece) for o in range(L - piece, -1, -piece)]
+                for j in range(n)]
+
+    def reverse_strip(x):  # the byte order the reversed iovec lists present
+        return x.reshape(x.shape[:-1] + (L // piece, piece))[..., ::-1, :].reshape(x.shape)
+
+    ctx = ec.Ctx()
+    try:
+        s0 = 0
+        for nb in batches:
+            for s in range(s0, s0 + nb):
+                assert ctx.encode_sg(k, m, strips(s), L) == 0
+            ctx.flush()
+            s0 += nb
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    got = reverse_strip(buf.cpu().numpy())
+    assert (got == oracle_encode_np(got, k, m)).all()
