@@ -7,10 +7,10 @@
 //   raid5_chunk_map_iov raid5.c:358-426 (slicing a parent bdev_io's iovecs)
 // Here the same walk runs on the host but, instead of calling the arithmetic per
 // run, it appends each run to a gather-descriptor list (k+m device-accessible
-// pointers + a length).  draid_ec_ctx_flush() packs the queued descriptors of
-// each (op, k, m) group into pinned ring slots (about 1 MiB per piece), DMAs
-// each piece on a copy stream and launches one kernel per piece on the compute
-// stream, so uploads overlap kernels.  A context is single-threaded, like an
+// pointers, written straight into pinned memory, + a length).
+// draid_ec_ctx_flush() DMAs the queued descriptors of each (op, k, m) group in
+// pieces of about 1 MiB on a copy stream and launches one kernel per piece on
+// the compute stream, so uploads overlap kernels.  A context is single-threaded, like an
 // SPDK io_channel: one per reactor thread.
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
@@ -76,7 +76,7 @@ private:
 };
 
 struct Group {
-    Group(int op_, uint32_t k_, uint32_t m_) : op(op_), k(k_), m(m_) {}
+    Group(int op_, uint32_t k_, uint32_t m_) : op(op_), k(k_), m(m_), w(k_ + m_ + (op_ == 1)) {}
     Group(const Group&) = delete;
     Group& operator=(const Group&) = delete;
     ~Group()
@@ -87,9 +87,11 @@ struct Group {
     }
     int op;  // 0 encode, 1 reconstruct, 2 read-modify-write update
     uint32_t k, m;                  // op 2: k = 2 * touched chunks (old/new list pairs)
-    PinnedPtrs ptrs;                // [nseg][k+m]
+    uint32_t w;                     // pointer slots per segment: k+m, +1 for op 1
+    PinnedPtrs ptrs;                // [nseg][w]; op 1: slot k+m holds the failure pair
+                                    // in its first two bytes (uploaded with the pointers)
     std::vector<uint32_t> len;      // [nseg]
-    std::vector<uint8_t> fail;      // [nseg][2] failure pair (op 1) / [nseg][k/2] exponents (op 2)
+    std::vector<uint8_t> fail;      // op 2: [nseg][k/2] exponents
     // Double-buffered pointer storage: a flush whose pieces DMA straight from
     // `ptrs` records uploaded[0] behind those copies and swaps in `spare`, so the
     // next batch is walked while the copies run; a buffer is written again only
@@ -167,7 +169,7 @@ const uint32_t* address_order(draid_ec_ctx* c, const Group& g)
         bytes += l;
     if (!force && bytes * n < kOrderMinSegmentBytes * nseg)
         return nullptr;
-    auto key = [&](size_t s) { return reinterpret_cast<uintptr_t>(g.ptrs[s * n]); };
+    auto key = [&](size_t s) { return reinterpret_cast<uintptr_t>(g.ptrs[s * g.w]); };
     uintptr_t lo = key(0), hi = lo;
     bool local = true;
     for (size_t s = 1; s < nseg; ++s) {
@@ -297,7 +299,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             }
             run = std::min<size_t>(run, avail);
         }
-        const void** out = g.ptrs.grow(n);
+        const void** out = g.ptrs.grow(g.w);
         if (!out)
             return rollback("out of pinned host memory for descriptors");
         for (uint32_t j = 0; j < n; ++j) {
@@ -317,8 +319,13 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             t.left -= r;
         }
         g.len.push_back(static_cast<uint32_t>(run));
-        if (nmeta)
+        if (op == 1) {  // failure pair into the row's spare slot
+            uintptr_t f = 0;
+            memcpy(&f, meta, 2);
+            out[n] = reinterpret_cast<const void*>(f);
+        } else if (nmeta) {
             g.fail.insert(g.fail.end(), meta, meta + nmeta);
+        }
         ++c->queued_segments;
         remaining -= run;
     }
@@ -371,7 +378,8 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
         return ctx_arg("flush: too many work items queued (flush more often)");
     const uint32_t nwork = static_cast<uint32_t>(nwork64);
     const size_t o_ptr = 0;
-    const size_t o_len = align8(o_ptr + nseg * n * sizeof(void*));
+    const uint32_t w = g.w;
+    const size_t o_len = align8(o_ptr + nseg * w * sizeof(void*));
     const size_t o_fail = align8(o_len + (uniform ? 0 : nseg * sizeof(uint32_t)));
     const size_t o_work = align8(o_fail + nseg * nmeta);
     const size_t bytes = o_work + work.size() * sizeof(uint32_t);
@@ -402,7 +410,7 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     if (perm) {
         auto* hp = reinterpret_cast<const void**>(h + o_ptr);
         for (size_t i = 0; i < nseg; ++i)
-            memcpy(hp + i * n, g.ptrs.data() + (size_t)perm[s0 + i] * n, n * sizeof(void*));
+            memcpy(hp + i * w, g.ptrs.data() + (size_t)perm[s0 + i] * w, w * sizeof(void*));
         for (size_t i = 0; nmeta && i < nseg; ++i)
             memcpy(h + o_fail + i * nmeta, g.fail.data() + (size_t)perm[s0 + i] * nmeta, nmeta);
     } else if (nmeta) {
@@ -421,8 +429,8 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     if (perm)
         e = hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, c->copy);
     else {
-        e = hipMemcpyAsync(static_cast<uint8_t*>(sl.dev) + o_ptr, g.ptrs.data() + s0 * n,
-                           nseg * n * sizeof(void*), hipMemcpyHostToDevice, c->copy);
+        e = hipMemcpyAsync(static_cast<uint8_t*>(sl.dev) + o_ptr, g.ptrs.data() + s0 * w,
+                           nseg * w * sizeof(void*), hipMemcpyHostToDevice, c->copy);
         if (e == hipSuccess && bytes > o_len)
             e = hipMemcpyAsync(static_cast<uint8_t*>(sl.dev) + o_len, h + o_len, bytes - o_len,
                                hipMemcpyHostToDevice, c->copy);
@@ -441,7 +449,10 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     if (g.op == 0)
         e = draid::launch_encode_work(g.k, g.m, tab, lens, wl, ulen, nwork, c->stream);
     else if (g.op == 1)
-        e = draid::launch_reconstruct_work(g.k, g.m, tab, lens, d + o_fail, wl, ulen, nwork,
+        e = draid::launch_reconstruct_work(g.k, g.m, tab, w, lens,
+                                           d + o_ptr + n * sizeof(void*),
+                                           static_cast<uint32_t>(w * sizeof(void*)), wl, ulen,
+                                           nwork,
                                            c->stream);
     else
         e = draid::launch_update_work(g.m, g.k / 2, tab, d + o_fail, lens, wl, ulen, nwork,
@@ -469,9 +480,12 @@ int flush_single(draid_ec_ctx* c, Group& g)
     hipError_t e;
     if (g.op == 0)
         e = draid::launch_encode(g.k, g.m, g.len[0], 1, nullptr, &args, c->stream);
-    else
-        e = draid::launch_reconstruct(g.k, g.m, g.len[0], 1, nullptr, &args, nullptr, g.fail[0],
-                                      g.fail[1], c->stream);
+    else {
+        uint8_t f[sizeof(void*)];
+        memcpy(f, &g.ptrs.data()[n], sizeof(f));  // the row's failure-pair slot
+        e = draid::launch_reconstruct(g.k, g.m, g.len[0], 1, nullptr, &args, nullptr, f[0], f[1],
+                                      c->stream);
+    }
     g.ptrs.clear();
     g.len.clear();
     g.fail.clear();
@@ -485,7 +499,7 @@ int flush_group(draid_ec_ctx* c, Group& g)
         return 0;
     if (nseg == 1 && g.op != 2 && g.k + g.m <= static_cast<uint32_t>(draid::kMaxArgPtrs))
         return flush_single(c, g);
-    const size_t per_seg = (g.k + g.m) * sizeof(void*) + sizeof(uint32_t) + 2 * sizeof(uint32_t);
+    const size_t per_seg = g.w * sizeof(void*) + sizeof(uint32_t) + 2 * sizeof(uint32_t);
     const size_t piece = std::max<size_t>(kMinPieceSegments, kPieceBytes / per_seg);
     const uint32_t* perm = address_order(c, g);
     int rc = 0;

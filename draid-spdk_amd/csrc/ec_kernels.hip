@@ -657,7 +657,7 @@ __global__ __launch_bounds__(C::NTHR) void k_encode_work(TablePtrs pp, uint32_t 
 template <int KT, int M, class C>
 __global__ __launch_bounds__(C::NTHR) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
                                                               WorkSrc ws, const uint8_t* fail,
-                                                              uint32_t nwork)
+                                                              uint32_t fstride, uint32_t nwork)
 {
     __shared__ LdsGf lds;
     const uint8_t* l_exp = reinterpret_cast<const uint8_t*>(lds.w);
@@ -669,7 +669,8 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct_work(TablePtrs pp, uint
     for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
         uint32_t seg, chunk, len, cps;
         ws.get(b, CB, seg, chunk, len, cps);
-        RecPlan pl = decode_failures<M>(k, fail[2 * (size_t)seg], fail[2 * (size_t)seg + 1]);
+        const uint8_t* f = fail + static_cast<size_t>(fstride) * seg;
+        RecPlan pl = decode_failures<M>(k, f[0], f[1]);
         if (pl.skip)
             continue;
         reconstruct_item<KT, M, C>(pp, seg, chunk, k, len, cps, pl, [&](RecPlan& p) {
@@ -1117,15 +1118,16 @@ static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, const ui
 }
 
 template <int KT, int M, class C>
-static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t k,
+static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t tstride, uint32_t k,
                                       const uint32_t* seg_len, const uint8_t* fail,
-                                      const void* work, uint32_t ulen, uint32_t nwork,
-                                      hipStream_t st)
+                                      uint32_t fstride, const void* work, uint32_t ulen,
+                                      uint32_t nwork, hipStream_t st)
 {
     if (nwork == 0)
         return hipSuccess;
     hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                       TablePtrs{tab, k + M}, k, work_src<C>(seg_len, work, ulen), fail, nwork);
+                       TablePtrs{tab, tstride}, k, work_src<C>(seg_len, work, ulen), fail,
+                       fstride, nwork);
     return hipGetLastError();
 }
 
@@ -1168,23 +1170,24 @@ hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* tabl
 }
 
 hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
-                                   const uint32_t* seg_len, const uint8_t* fail, const void* work,
-                                   uint32_t ulen, uint32_t nwork, hipStream_t st)
+                                   uint32_t tstride, const uint32_t* seg_len, const uint8_t* fail,
+                                   uint32_t fstride, const void* work, uint32_t ulen,
+                                   uint32_t nwork, hipStream_t st)
 {
     switch (k) {
 #define DRAID_CASE(K)                                                                         \
     case K:                                                                                   \
         return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K)>>(                 \
-                            table, k, seg_len, fail, work, ulen, nwork, st)                  \
+                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st) \
                       : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K)>>(                 \
-                            table, k, seg_len, fail, work, ulen, nwork, st);
+                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return m == 1 ? go_reconstruct_work<0, 1, RecCfg<2>>(table, k, seg_len, fail, work,
-                                                                 ulen, nwork, st)
-                      : go_reconstruct_work<0, 2, RecCfg<2>>(table, k, seg_len, fail, work,
-                                                                 ulen, nwork, st);
+        return m == 1 ? go_reconstruct_work<0, 1, RecCfg<2>>(table, tstride, k, seg_len, fail,
+                                                                 fstride, work, ulen, nwork, st)
+                      : go_reconstruct_work<0, 2, RecCfg<2>>(table, tstride, k, seg_len, fail,
+                                                                 fstride, work, ulen, nwork, st);
     }
 }
 
