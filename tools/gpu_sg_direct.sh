@@ -12,7 +12,7 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout
 tail -1 gpurun_out/pytest_sg.log
 out=gpurun_out/sg_direct_ab.jsonl
 rm -f $out
-for round in 1 2; do
+for round in 1 2 3; do
   for a in "65536 0" "4096 0" "1024 0" "65536 1024" "4096 4096"; do
     set -- $a
     for lib in old new; do
