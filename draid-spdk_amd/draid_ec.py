@@ -19,6 +19,7 @@ LAB_LIB_PATH = os.path.join(HERE, "liblab", "libdraid_ec.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "draid_ec.h")
 
 FAIL_NONE = 0xFF
+PQ_CHECK_STATIC_MAX_VECTS = 257  # DRAID_PQ_CHECK_STATIC_MAX_VECTS
 
 # Every symbol include/draid_ec.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -35,6 +36,7 @@ EXPORTS = (
     "draid_ec_ctx_queued", "draid_ec_host_encode", "draid_ec_host_reconstruct",
     "draid_ec_encode_strided", "draid_ec_reconstruct_strided",
     "draid_ec_ctx_update_sg", "draid_ec_host_device_pointer", "draid_ec_ctx_set_autoflush",
+    "draid_pq_check_static",
 )
 
 
@@ -84,6 +86,8 @@ def lib() -> C.CDLL:
         for f in ("draid_xor_gen", "draid_pq_gen", "draid_xor_check", "draid_pq_check"):
             getattr(L, f).argtypes = [i32, i32, C.POINTER(vp)]
             getattr(L, f).restype = i32
+        L.draid_pq_check_static.argtypes = [i32, i32, C.POINTER(vp), vp, vp]
+        L.draid_pq_check_static.restype = i32
         L.draid_gf_mul.argtypes = [u8, u8]
         L.draid_gf_mul.restype = u8
         L.draid_gf_inv.argtypes = [u8]
@@ -162,6 +166,12 @@ def xor_check(ptrs, length: int) -> int:
 
 def pq_check(ptrs, length: int) -> int:
     return _check(lib().draid_pq_check(len(ptrs), length, _array(ptrs)), "pq_check")
+
+
+def pq_check_static(ptrs, length: int, result_ptr, stream: int) -> int:
+    """Allocation-free draid_pq_check: enqueues on `stream`, verdict to *result_ptr."""
+    return _check(lib().draid_pq_check_static(len(ptrs), length, _array(ptrs), _ptr(result_ptr),
+                                              stream), "pq_check_static")
 
 
 def gf_mul(a: int, b: int) -> int:

@@ -66,6 +66,24 @@ int draid_xor_check(int vects, int len, void **array);
  * (isa-l pq_check(); used at gf_vect_mul.c:178-179). */
 int draid_pq_check(int vects, int len, void **array);
 
+/* draid_pq_check() for callers that cannot allocate.  No counterpart in the
+ * reference: it exists for callers that may not call hipMalloc -- code under HIP
+ * graph capture, tight scrub loops, harnesses that forbid allocation.
+ * draid_pq_check() keeps its mismatch flag and (above 34 vectors) its pointer
+ * table in device memory it allocates on first use; this variant keeps both in
+ * a 4 KiB static device array inside the library (one copy per GPU, held until
+ * the process ends) and allocates, frees and copies nothing.
+ * Same arguments and argument errors as draid_pq_check(), plus:
+ *   vects  at most DRAID_PQ_CHECK_STATIC_MAX_VECTS (the static table), else 1;
+ *   result device-accessible word (device memory, or the device address of
+ *          pinned / registered host memory); receives 0 if P and Q match, 1 if not;
+ *   stream the work is enqueued here and the call returns without waiting:
+ *          *result is valid once the stream has finished.
+ * Every call on a GPU shares that GPU's array: calls that overlap in time on
+ * one GPU (other streams or threads) race and may report the wrong verdict. */
+#define DRAID_PQ_CHECK_STATIC_MAX_VECTS 257 /* k = 255 data strips + P + Q */
+int draid_pq_check_static(int vects, int len, void **array, uint32_t *result, void *stream);
+
 /* GF(2^8) scalar helpers (host-side; isa-l erasure_code.h gf_mul / gf_inv,
  * gf_vect_mul.h gf_vect_mul_init -- gf_vect_mul.c:60-66,313-322). */
 unsigned char draid_gf_mul(unsigned char a, unsigned char b);
