@@ -161,6 +161,9 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="raid6_8p2_64k", choices=sorted(CONFIGS))
+    ap.add_argument("--shape", default=None, metavar="K,M,STRIP_KIB,STRIPES,FAILURES",
+                    help="lab runs only: any stripe shape instead of a BASELINE config, "
+                         "e.g. 6,2,64,4096,dual (never the driver's bench line)")
     ap.add_argument("--stripes", type=int, default=None,
                     help="stripes per GPU (override); with --strong, the whole job's")
     ap.add_argument("--strong", action="store_true",
@@ -202,6 +205,11 @@ def main() -> None:
     ec.set_variant(args.variant)
 
     cfg = CONFIGS[args.config]
+    if args.shape:
+        sk, sm, skib, sb, sf = args.shape.split(",")
+        args.config = f"shape_{sk}p{sm}_{skib}k_{sf}"
+        cfg = dict(k=int(sk), m=int(sm), strip_kib=int(skib), stripes=int(sb), failures=sf,
+                   label=f"lab shape {sk}+{sm} x {skib} KiB, {sf} failure")
     k, m, S = cfg["k"], cfg["m"], cfg["strip_kib"] * 1024
     if args.strong:  # fixed total, contiguous stripe ranges per rank
         total = args.stripes or cfg.get("strong_stripes", cfg["stripes"])

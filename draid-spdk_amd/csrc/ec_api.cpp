@@ -26,6 +26,10 @@ thread_local char t_err[256] = "";
 namespace draid {
 int fail_hip(hipError_t e, const char* what)
 {
+    // The runtime keeps a failed call's code as the thread's "last error" until
+    // somebody reads it: clear it, or the next HIP user in the process (torch
+    // checks after every launch) reports this library's error as its own.
+    (void)hipGetLastError();
     snprintf(t_err, sizeof(t_err), "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
     return -static_cast<int>(e == hipSuccess ? 1 : e);
 }
@@ -45,24 +49,134 @@ namespace {
 hipStream_t sync_stream() { return hipStreamPerThread; }
 
 // Per-thread device scratch: a pointer table for calls with more vectors than
-// fit in kernel arguments, and a 4-byte flag for the *_check calls.
+// fit in kernel arguments, a 4-byte flag for the *_check calls, and a staging
+// arena for vectors in pageable host memory.
 struct Scratch {
     void* table = nullptr;
     size_t table_bytes = 0;
     uint32_t* flag = nullptr;
+    uint8_t* arena = nullptr;
+    size_t arena_bytes = 0;
     ~Scratch()
     {
         if (table)
             (void)hipFree(table);
         if (flag)
             (void)hipFree(flag);
+        if (arena)
+            (void)hipFree(arena);
     }
 };
 thread_local Scratch t_scratch;
 
+// The vectors of one synchronous call as a kernel may address them.
+//
+// isa-l works on whatever host memory it is given (raid5.c:188-201 passes
+// spdk_dma_malloc'd chunk buffers and user iovecs).  Here each vector is
+// resolved first (ec_xlate.cpp): device memory and pinned / registered host
+// memory are used in place, at their device addresses.  A vector in pageable
+// memory is never handed to a kernel -- that would be a GPU memory fault, which
+// ends the process instead of returning an error -- but staged: copied into a
+// per-thread device arena before the launch if the call reads it, and copied
+// back afterwards if the call writes it.  Equal host pointers share one staging
+// buffer, so in-place forms ({from, to, to}) keep their meaning.
+enum : uint8_t { kIn = 1, kOut = 2 };
+
+struct Vectors {
+    std::vector<void*> dev;  // what the kernel gets, per vector
+    struct Staged {
+        void* host;
+        size_t offset;
+        uint8_t use;
+    };
+    std::vector<Staged> staged;
+    size_t len = 0;
+
+    int resolve(void* const* host, const uint8_t* use, int n, size_t bytes)
+    {
+        dev.assign(static_cast<size_t>(n), nullptr);
+        staged.clear();
+        len = bytes;
+        size_t need = 0;
+        std::vector<int> slot(static_cast<size_t>(n), -1);
+        for (int i = 0; i < n; ++i) {
+            const void* d = nullptr;
+            if (draid::translate(host[i], bytes, &d) == 0) {
+                dev[i] = const_cast<void*>(d);
+                continue;
+            }
+            if (!host[i])
+                return fail_arg("a vector pointer is NULL");
+            for (size_t s = 0; s < staged.size(); ++s)
+                if (staged[s].host == host[i])
+                    slot[i] = static_cast<int>(s);
+            if (slot[i] < 0) {
+                slot[i] = static_cast<int>(staged.size());
+                staged.push_back({host[i], need, 0});
+                need += (bytes + 255) & ~size_t(255);
+            }
+            staged[slot[i]].use |= use[i];
+        }
+        if (staged.empty())
+            return 0;
+        if (t_scratch.arena_bytes < need) {
+            if (t_scratch.arena)
+                (void)hipFree(t_scratch.arena);
+            t_scratch.arena = nullptr;
+            t_scratch.arena_bytes = 0;
+            const hipError_t e = hipMalloc(&t_scratch.arena, need);
+            if (e != hipSuccess)
+                return fail_hip(e, "hipMalloc(staging for pageable vectors)");
+            t_scratch.arena_bytes = need;
+        }
+        for (int i = 0; i < n; ++i)
+            if (slot[i] >= 0)
+                dev[i] = t_scratch.arena + staged[slot[i]].offset;
+        for (const Staged& s : staged) {
+            if (!(s.use & kIn))
+                continue;
+            const hipError_t e = hipMemcpyAsync(t_scratch.arena + s.offset, s.host, bytes,
+                                                hipMemcpyHostToDevice, sync_stream());
+            if (e != hipSuccess)
+                return fail_hip(e, "hipMemcpyAsync(stage pageable vector in)");
+        }
+        return 0;
+    }
+
+    // Queues the copies back to pageable destinations (before the final wait).
+    hipError_t write_back() const
+    {
+        for (const Staged& s : staged) {
+            if (!(s.use & kOut))
+                continue;
+            const hipError_t e = hipMemcpyAsync(s.host, t_scratch.arena + s.offset, len,
+                                                hipMemcpyDeviceToHost, sync_stream());
+            if (e != hipSuccess)
+                return e;
+        }
+        return hipSuccess;
+    }
+};
+thread_local Vectors t_vec;
+
+// Resolves the n vectors of a stripe call whose last `nout` are written.
+int resolve_stripe(void** array, int n, int nout, size_t len)
+{
+    uint8_t use[kMaxArgPtrs];
+    std::vector<uint8_t> big;
+    uint8_t* u = use;
+    if (n > kMaxArgPtrs) {
+        big.resize(static_cast<size_t>(n));
+        u = big.data();
+    }
+    for (int i = 0; i < n; ++i)
+        u[i] = i < n - nout ? kIn : kOut;
+    return t_vec.resolve(array, u, n, len);
+}
+
 // Makes the pointers of one stripe available to a kernel: in kernel arguments
 // when they fit, else in the per-thread device table.
-int stage_pointers(void** array, int n, ArgPtrTable* args, const uint8_t* const** table)
+int stage_pointers(void* const* array, int n, ArgPtrTable* args, const uint8_t* const** table)
 {
     *table = nullptr;
     if (n <= kMaxArgPtrs) {
@@ -94,6 +208,9 @@ int finish_sync(hipError_t e, const char* what)
 {
     if (e != hipSuccess)
         return fail_hip(e, what);
+    e = t_vec.write_back();
+    if (e != hipSuccess)
+        return fail_hip(e, "hipMemcpyAsync(write staged vector back)");
     e = hipStreamSynchronize(sync_stream());
     if (e != hipSuccess)
         return fail_hip(e, "hipStreamSynchronize");
@@ -102,9 +219,13 @@ int finish_sync(hipError_t e, const char* what)
 
 int encode_one(uint32_t k, uint32_t m, int len, void** array)
 {
+    int rc = resolve_stripe(array, static_cast<int>(k + m), static_cast<int>(m),
+                            static_cast<size_t>(len));
+    if (rc)
+        return rc;
     ArgPtrTable args;
     const uint8_t* const* table;
-    int rc = stage_pointers(array, static_cast<int>(k + m), &args, &table);
+    rc = stage_pointers(t_vec.dev.data(), static_cast<int>(k + m), &args, &table);
     if (rc)
         return rc;
     return finish_sync(draid::launch_encode(k, m, static_cast<uint64_t>(len), 1, table,
@@ -119,9 +240,12 @@ int check_one(uint32_t k, uint32_t m, int len, void** array)
         if (e != hipSuccess)
             return fail_hip(e, "hipMalloc(flag)");
     }
+    int rc = resolve_stripe(array, static_cast<int>(k + m), 0, static_cast<size_t>(len));
+    if (rc)
+        return rc;
     ArgPtrTable args;
     const uint8_t* const* table;
-    int rc = stage_pointers(array, static_cast<int>(k + m), &args, &table);
+    rc = stage_pointers(t_vec.dev.data(), static_cast<int>(k + m), &args, &table);
     if (rc)
         return rc;
     hipError_t e = hipMemsetAsync(t_scratch.flag, 0, sizeof(uint32_t), sync_stream());
@@ -200,9 +324,13 @@ int draid_gf_vect_mul(int len, unsigned char* tbl, void* src, void* dest)
         return fail_arg("gf_vect_mul needs len % 32 == 0");
     if (len == 0)
         return 0;
+    void* v[2] = {src, dest};
+    const uint8_t use[2] = {kIn, kOut};
+    if (const int rc = t_vec.resolve(v, use, 2, static_cast<size_t>(len)))
+        return rc;
     return finish_sync(draid::launch_gf_vect_mul(static_cast<uint64_t>(len), tbl,
-                                                 static_cast<const uint8_t*>(src),
-                                                 static_cast<uint8_t*>(dest), sync_stream()),
+                                                 static_cast<const uint8_t*>(t_vec.dev[0]),
+                                                 static_cast<uint8_t*>(t_vec.dev[1]), sync_stream()),
                        "launch_gf_vect_mul");
 }
 
@@ -223,15 +351,21 @@ int draid_recover(int k, int m, int len, void** array, int nfail, const int* fai
     }
     if (nfail == 0 || len == 0)
         return 0;
+    std::vector<uint8_t> use(static_cast<size_t>(k + m), kIn);
+    for (int i = 0; i < nfail; ++i)
+        use[fail[i]] = kOut;
+    int rc = t_vec.resolve(array, use.data(), k + m, static_cast<size_t>(len));
+    if (rc)
+        return rc;
     ArgPtrTable args;
     const uint8_t* const* table;
-    int rc = stage_pointers(array, k + m, &args, &table);
+    rc = stage_pointers(t_vec.dev.data(), k + m, &args, &table);
     if (rc)
         return rc;
     return finish_sync(draid::launch_reconstruct(static_cast<uint32_t>(k), static_cast<uint32_t>(m),
                                                  static_cast<uint64_t>(len), 1, table,
                                                  table ? nullptr : &args, nullptr, f[0], f[1],
-                                                 sync_stream()),
+                                                 nullptr, sync_stream()),
                        "launch_reconstruct");
 }
 
@@ -264,6 +398,12 @@ int draid_ec_encode(const draid_ec_stripe_batch* b, void* stream)
 
 int draid_ec_reconstruct(const draid_ec_stripe_batch* b, const uint8_t* fail, void* stream)
 {
+    return draid_ec_reconstruct_status(b, fail, nullptr, stream);
+}
+
+int draid_ec_reconstruct_status(const draid_ec_stripe_batch* b, const uint8_t* fail,
+                                uint32_t* unrecoverable, void* stream)
+{
     int rc = check_batch(b);
     if (rc || !b->nstripes || !b->strip_len)
         return rc;
@@ -273,7 +413,8 @@ int draid_ec_reconstruct(const draid_ec_stripe_batch* b, const uint8_t* fail, vo
         return fail_arg("reconstruct: fail table is NULL");
     hipError_t e = draid::launch_reconstruct(
         b->k, b->m, b->strip_len, b->nstripes, reinterpret_cast<const uint8_t* const*>(b->strips),
-        nullptr, fail, DRAID_EC_FAIL_NONE, DRAID_EC_FAIL_NONE, static_cast<hipStream_t>(stream));
+        nullptr, fail, DRAID_EC_FAIL_NONE, DRAID_EC_FAIL_NONE, unrecoverable,
+        static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : fail_hip(e, "launch_reconstruct");
 }
 
@@ -306,6 +447,12 @@ int draid_ec_encode_strided(const draid_ec_strided_stripes* d, void* stream)
 int draid_ec_reconstruct_strided(const draid_ec_strided_stripes* d, const uint8_t* fail,
                                  void* stream)
 {
+    return draid_ec_reconstruct_strided_status(d, fail, nullptr, stream);
+}
+
+int draid_ec_reconstruct_strided_status(const draid_ec_strided_stripes* d, const uint8_t* fail,
+                                        uint32_t* unrecoverable, void* stream)
+{
     int rc = check_strided(d);
     if (rc || !d->nstripes || !d->strip_len)
         return rc;
@@ -315,7 +462,7 @@ int draid_ec_reconstruct_strided(const draid_ec_strided_stripes* d, const uint8_
         return fail_arg("reconstruct: fail table is NULL");
     hipError_t e = draid::launch_reconstruct_strided(
         d->k, d->m, d->strip_len, d->nstripes, static_cast<const uint8_t*>(d->base),
-        d->strip_stride, d->stripe_stride, fail, static_cast<hipStream_t>(stream));
+        d->strip_stride, d->stripe_stride, fail, unrecoverable, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : fail_hip(e, "launch_reconstruct_strided");
 }
 
@@ -383,6 +530,7 @@ int draid_ec_device_alloc(void** ptr, size_t bytes)
 
 int draid_ec_device_free(void* ptr)
 {
+    draid::translate_invalidate();  // cached ranges may name this memory
     hipError_t e = hipFree(ptr);
     return e == hipSuccess ? 0 : fail_hip(e, "hipFree");
 }
@@ -395,6 +543,7 @@ int draid_ec_host_register(void* ptr, size_t bytes)
 
 int draid_ec_host_unregister(void* ptr)
 {
+    draid::translate_invalidate();  // cached ranges may name this memory
     hipError_t e = hipHostUnregister(ptr);
     return e == hipSuccess ? 0 : fail_hip(e, "hipHostUnregister");
 }

@@ -86,6 +86,7 @@ struct Group {
                 (void)hipEventDestroy(e);
     }
     int op;  // 0 encode, 1 reconstruct, 2 read-modify-write update
+    uint64_t first_seq = 0;         // queue position of the batch's first segment in this group
     uint32_t k, m;                  // op 2: k = 2 * touched chunks (old/new list pairs)
     uint32_t w;                     // pointer slots per segment: k+m, +1 for op 1
     PinnedPtrs ptrs;                // [nseg][w]; op 1: slot k+m holds the failure pair
@@ -139,7 +140,41 @@ struct draid_ec_ctx {
                             // (diagnostics and tests)
     std::vector<uint32_t> perm, bucket;
     uint64_t autoflush = 0;  // launch a group once it holds this many segments (0 = off)
+    uint64_t seq = 0;        // segments queued so far (orders the groups of a flush)
+    bool host_pointers = false;  // iov_base values are the caller's host addresses: resolve them
+    int fail_after = 0;      // test hook: the n-th piece from now fails before it launches
+    // Flush tickets: an event recorded behind each ticketed flush, so a poller can
+    // complete the requests of one flush while later ones are still running.
+    static constexpr uint64_t kTickets = 64;
+    hipEvent_t ticket_ev[kTickets] = {};
+    uint64_t ticket_next = 1, ticket_done = 0;
 };
+
+namespace {
+// Work on a context's streams is issued with its device current.
+struct DeviceGuard {
+    int prev = -1;
+    bool switched = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev)
+            switched = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard()
+    {
+        if (switched)
+            (void)hipSetDevice(prev);
+    }
+};
+
+void recount(draid_ec_ctx* c)
+{
+    uint64_t n = 0;
+    for (const Group& g : c->groups)
+        n += g.len.size();
+    c->queued_segments = n;
+}
+}  // namespace
 
 namespace {
 
@@ -211,14 +246,32 @@ struct IovIter {
     const struct iovec* v;
     int cnt;
     int idx;
-    const uint8_t* p;  // current byte
+    const uint8_t* p;  // current byte (the caller's address)
     size_t left;       // bytes left in v[idx] from p
+    intptr_t delta;    // device address = p + delta (0 unless the ctx resolves host pointers)
+    bool xl;           // resolve each iovec (draid_ec_ctx_set_host_pointers)
+    bool bad;          // an iovec was not GPU accessible
+
+    // Device-address offset of one iovec, or false when the GPU cannot reach it.
+    static bool resolve(const struct iovec& e, intptr_t* d)
+    {
+        *d = 0;
+        if (e.iov_len == 0)
+            return true;
+        const void* dev = nullptr;
+        if (draid::translate(e.iov_base, e.iov_len, &dev))
+            return false;
+        *d = static_cast<const uint8_t*>(dev) - static_cast<const uint8_t*>(e.iov_base);
+        return true;
+    }
 
     void enter(int i)
     {
         idx = i;
         p = static_cast<const uint8_t*>(v[i].iov_base);
         left = v[i].iov_len;
+        if (xl && !resolve(v[i], &delta))
+            bad = true;
     }
 };
 
@@ -253,9 +306,12 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     for (uint32_t j = 0; j < n; ++j) {
         if (!iovs || !iovs[j] || !iovcnt || iovcnt[j] < 0)
             return ctx_arg("iovec list missing");
-        it[j] = IovIter{iovs[j], iovcnt[j], 0, nullptr, 0};
+        it[j] = IovIter{iovs[j], iovcnt[j], 0, nullptr, 0, 0, c->host_pointers, false};
         if (len && !iter_seek(it[j], offset ? offset[j] : 0))
             return ctx_arg("iovec list shorter than offset");
+        if (it[j].bad)
+            return ctx_arg("an iovec is neither device memory nor pinned / registered host "
+                           "memory");
     }
     Group& g = group_for(c, op, k, m);
     if (const int rc = g.ready())
@@ -294,17 +350,29 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                     continue;
                 if (t.v[x].iov_base != end)
                     break;
+                if (t.xl) {  // adjacent for the host: also adjacent for the device?
+                    intptr_t d;
+                    if (!IovIter::resolve(t.v[x], &d) || d != t.delta)
+                        break;
+                }
                 avail += t.v[x].iov_len;
                 end += t.v[x].iov_len;
             }
             run = std::min<size_t>(run, avail);
         }
+        for (uint32_t j = 0; j < n; ++j)
+            if (it[j].bad)
+                return rollback("an iovec is neither device memory nor pinned / registered host "
+                                "memory");
+        if (g.len.empty())
+            g.first_seq = c->seq;
+        ++c->seq;
         const void** out = g.ptrs.grow(g.w);
         if (!out)
             return rollback("out of pinned host memory for descriptors");
         for (uint32_t j = 0; j < n; ++j) {
             IovIter& t = it[j];
-            out[j] = t.p;
+            out[j] = t.p + t.delta;
             if (run <= t.left) {
                 t.p += run;
                 t.left -= run;
@@ -330,9 +398,9 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
         remaining -= run;
     }
     if (c->autoflush && g.len.size() >= c->autoflush) {
-        const size_t nseg = g.len.size();
+        DeviceGuard on(c->device);
         const int rc = flush_group(c, g);
-        c->queued_segments -= nseg;
+        recount(c);
         return rc;
     }
     return 0;
@@ -345,6 +413,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
 // `perm` (may be null): segment i of the group is g's segment perm[i].
 int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size_t s1)
 {
+    if (c->fail_after > 0 && --c->fail_after == 0)
+        return ctx_fail(hipErrorOutOfMemory, "flush piece (injected failure)");
     const size_t nseg = s1 - s0;
     const uint32_t n = g.k + g.m;
     const size_t nmeta = g.fail.size() / g.len.size();  // bytes of meta per segment
@@ -484,7 +554,7 @@ int flush_single(draid_ec_ctx* c, Group& g)
         uint8_t f[sizeof(void*)];
         memcpy(f, &g.ptrs.data()[n], sizeof(f));  // the row's failure-pair slot
         e = draid::launch_reconstruct(g.k, g.m, g.len[0], 1, nullptr, &args, nullptr, f[0], f[1],
-                                      c->stream);
+                                      nullptr, c->stream);
     }
     g.ptrs.clear();
     g.len.clear();
@@ -504,8 +574,39 @@ int flush_group(draid_ec_ctx* c, Group& g)
     const uint32_t* perm = address_order(c, g);
     int rc = 0;
     g.direct = false;
-    for (size_t s0 = 0; s0 < nseg && rc == 0; s0 += piece)
+    size_t launched = 0;
+    for (size_t s0 = 0; s0 < nseg; s0 += piece) {
         rc = flush_piece(c, g, perm, s0, std::min(nseg, s0 + piece));
+        if (rc)
+            break;
+        launched = std::min(nseg, s0 + piece);
+    }
+    if (rc && launched < nseg) {
+        // A piece failed (descriptor memory, the work-item limit, a launch error):
+        // the pieces before it are running, this one and the rest are not.  Keep
+        // exactly those segments queued, in their queue order, so the caller can
+        // flush again or fail precisely the requests that did not run.
+        (void)hipStreamSynchronize(c->copy);  // nothing may still read g.ptrs
+        g.pending[0] = g.pending[1] = false;
+        std::vector<uint32_t> rest;
+        rest.reserve(nseg - launched);
+        for (size_t i = launched; i < nseg; ++i)
+            rest.push_back(perm ? perm[i] : static_cast<uint32_t>(i));
+        std::sort(rest.begin(), rest.end());
+        const size_t nmeta = g.fail.size() / nseg;
+        const void** rows = g.ptrs.data();
+        for (size_t i = 0; i < rest.size(); ++i) {  // rest[i] >= i: forward moves are safe
+            memmove(rows + i * g.w, rows + static_cast<size_t>(rest[i]) * g.w,
+                    g.w * sizeof(void*));
+            g.len[i] = g.len[rest[i]];
+            if (nmeta)
+                memmove(g.fail.data() + i * nmeta, g.fail.data() + rest[i] * nmeta, nmeta);
+        }
+        g.ptrs.shrink(rest.size() * g.w);
+        g.len.resize(rest.size());
+        g.fail.resize(rest.size() * nmeta);
+        return rc;
+    }
     if (g.direct) {  // copies from g.ptrs in flight: walk the next batch into the spare
         hipError_t e = hipSuccess;
         if (!g.uploaded[0])
@@ -553,6 +654,8 @@ int draid_ec_ctx_create(draid_ec_ctx** out)
         if (e == hipSuccess)
             e = hipEventCreateWithFlags(&c->slots[i].uploaded, hipEventDisableTiming);
     }
+    for (uint64_t i = 0; e == hipSuccess && i < draid_ec_ctx::kTickets; ++i)
+        e = hipEventCreateWithFlags(&c->ticket_ev[i], hipEventDisableTiming);
     if (e != hipSuccess) {
         int rc = ctx_fail(e, "draid_ec_ctx_create");
         draid_ec_ctx_destroy(c);
@@ -566,8 +669,12 @@ int draid_ec_ctx_destroy(draid_ec_ctx* c)
 {
     if (!c)
         return 0;
+    DeviceGuard on(c->device);
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
+    for (hipEvent_t ev : c->ticket_ev)
+        if (ev)
+            (void)hipEventDestroy(ev);
     if (c->copy)
         (void)hipStreamSynchronize(c->copy);
     for (Slot& s : c->slots) {
@@ -658,13 +765,88 @@ int draid_ec_ctx_flush(draid_ec_ctx* c)
 {
     if (!c)
         return ctx_arg("ctx is NULL");
-    for (Group& g : c->groups) {
-        int rc = flush_group(c, g);
-        if (rc)
-            return rc;
+    DeviceGuard on(c->device);
+    // Groups launch in the order their first segment of this batch was queued
+    // (a group object outlives its batches, so creation order says nothing).
+    Group* order[64];
+    std::vector<Group*> many;
+    size_t n = 0;
+    for (Group& g : c->groups)
+        if (!g.len.empty()) {
+            if (n < 64)
+                order[n] = &g;
+            else {
+                if (many.empty())
+                    many.assign(order, order + 64);
+                many.push_back(&g);
+            }
+            ++n;
+        }
+    Group** gp = many.empty() ? order : many.data();
+    std::sort(gp, gp + n, [](const Group* a, const Group* b) { return a->first_seq < b->first_seq; });
+    int rc = 0;
+    for (size_t i = 0; i < n && rc == 0; ++i)
+        rc = flush_group(c, *gp[i]);
+    recount(c);  // on failure: exactly the segments that did not launch
+    return rc;
+}
+
+int draid_ec_ctx_flush_ticket(draid_ec_ctx* c, uint64_t* ticket)
+{
+    if (!c || !ticket)
+        return ctx_arg("flush_ticket needs a ctx and a ticket pointer");
+    *ticket = 0;
+    const int rc = draid_ec_ctx_flush(c);
+    if (rc)
+        return rc;
+    DeviceGuard on(c->device);
+    const uint64_t t = c->ticket_next;
+    hipError_t e;
+    if (t - c->ticket_done > draid_ec_ctx::kTickets) {  // the event slot is still in use
+        const uint64_t old = t - draid_ec_ctx::kTickets;
+        if ((e = hipEventSynchronize(c->ticket_ev[old % draid_ec_ctx::kTickets])) != hipSuccess)
+            return ctx_fail(e, "hipEventSynchronize(ticket)");
+        c->ticket_done = old;
     }
-    c->queued_segments = 0;
+    if ((e = hipEventRecord(c->ticket_ev[t % draid_ec_ctx::kTickets], c->stream)) != hipSuccess)
+        return ctx_fail(e, "hipEventRecord(ticket)");
+    c->ticket_next = t + 1;
+    *ticket = t;
     return 0;
+}
+
+int draid_ec_ctx_ticket_query(draid_ec_ctx* c, uint64_t ticket)
+{
+    if (!c || ticket == 0 || ticket >= c->ticket_next)
+        return ctx_arg("ticket_query: not a ticket of this context");
+    if (ticket <= c->ticket_done)
+        return 0;
+    const hipError_t e = hipEventQuery(c->ticket_ev[ticket % draid_ec_ctx::kTickets]);
+    if (e == hipSuccess) {
+        c->ticket_done = ticket;  // stream order: every earlier flush is done too
+        return 0;
+    }
+    if (e == hipErrorNotReady) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    return ctx_fail(e, "hipEventQuery(ticket)");
+}
+
+int draid_ec_ctx_set_host_pointers(draid_ec_ctx* c, int on)
+{
+    if (!c)
+        return ctx_arg("ctx is NULL");
+    c->host_pointers = on != 0;
+    return 0;
+}
+
+// Test hook (not in the public header): the n-th piece launched from now on
+// fails before it does anything, as a descriptor allocation failure would.
+void draid_ec_ctx_test_fail_after(draid_ec_ctx* c, int n)
+{
+    if (c)
+        c->fail_after = n;
 }
 
 int draid_ec_ctx_query(draid_ec_ctx* c)
@@ -674,8 +856,10 @@ int draid_ec_ctx_query(draid_ec_ctx* c)
     hipError_t e = hipStreamQuery(c->stream);
     if (e == hipSuccess)
         return 0;
-    if (e == hipErrorNotReady)
+    if (e == hipErrorNotReady) {
+        (void)hipGetLastError();
         return 1;
+    }
     return ctx_fail(e, "hipStreamQuery");
 }
 

@@ -47,18 +47,28 @@ inline uint8_t gf_mul_host(uint8_t a, uint8_t b)
 }
 inline uint8_t gf_inv_host(uint8_t a) { return a ? kGfHost.exp[255 - kGfHost.log[a]] : 0; }
 
-// ---- device: multiply every byte by 2 (SWAR, isa-l pq_gen_base word form) ----
+// ---- device: multiply every byte by 2 (isa-l pq_gen_base word form) ----
+// Per byte: (q << 1) ^ (bit 7 set ? 0x1d : 0).  The reduction byte is looked up
+// with one v_perm_b32 whose selector is the byte's top bit (entry 0 = 0x00,
+// entry 1 = 0x1d): 6 VALU ops per dword (shift, and, perm, shift, and, xor)
+// against 8 for the shift-and-subtract mask form.  The reconstruct of a narrow
+// stripe is VALU-sensitive: when the shader clock dips under a fresh memory load
+// (2.4 -> 1.6 GHz for the first ~10 ms after an idle gap, tools/probe/
+// transient_probe.hip) a kernel near the VALU limit slows down with it.
 __device__ __forceinline__ uint32_t gf_mul2(uint32_t q)
 {
-    const uint32_t hi = q & 0x80808080u;
-    const uint32_t mask = (hi << 1) - (hi >> 7);  // 0xFF in every byte whose bit 7 is set
-    return ((q & 0x7f7f7f7fu) << 1) ^ (mask & 0x1d1d1d1du);
+    const uint32_t top = (q >> 7) & 0x01010101u;
+    const uint32_t red = __builtin_amdgcn_perm(0u, 0x00001d00u, top);
+    return ((q << 1) & 0xfefefefeu) ^ red;
 }
 __device__ __forceinline__ u32x4 gf_mul2(u32x4 q)
 {
-    const u32x4 hi = q & 0x80808080u;
-    const u32x4 mask = (hi << 1) - (hi >> 7);
-    return ((q & 0x7f7f7f7fu) << 1) ^ (mask & 0x1d1d1d1du);
+    u32x4 r;
+    r.x = gf_mul2(q.x);
+    r.y = gf_mul2(q.y);
+    r.z = gf_mul2(q.z);
+    r.w = gf_mul2(q.w);
+    return r;
 }
 
 // ---- device: multiply by a constant c through isa-l's 32-byte nibble table ----
@@ -120,6 +130,60 @@ __device__ __forceinline__ uint32_t gf_mulc(const NibTable& t, uint32_t x)
     return lut16(t.lo, x & 0x0f0f0f0fu) ^ lut16(t.hi, (x >> 4) & 0x0f0f0f0fu);
 }
 __device__ __forceinline__ u32x4 gf_mulc(const NibTable& t, u32x4 x)
+{
+    u32x4 r;
+    r.x = gf_mulc(t, x.x);
+    r.y = gf_mulc(t, x.y);
+    r.z = gf_mulc(t, x.z);
+    r.w = gf_mulc(t, x.w);
+    return r;
+}
+
+// ---- device: multiply by a wave-uniform constant through 3-bit tables ----
+// c * x is linear over GF(2), so x splits into bits 0-2, 3-5 and 6-7 and
+//   c * x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6],
+// with T0[r] = c*r, T1[r] = c*(r << 3), T2[r] = c*(r << 6).  An 8-entry byte
+// table is one register pair, so each term is a single v_perm_b32 with the
+// 3-bit field as selector: 9 VALU ops per dword (two shifts, three ands, three
+// perms, one three-way xor) against 22 for the two 16-entry nibble lookups.
+// The 20 table bytes are built on the SALU from the constant (closed form).
+struct MulTable {
+    uint32_t t0[2];  // bytes c*0 .. c*7
+    uint32_t t1[2];  // bytes c*(0<<3) .. c*(7<<3)
+    uint32_t t2;     // bytes c*(0<<6) .. c*(3<<6)
+};
+
+// Entries r = 0..7 over the three basis products (pa, pb, pc) = c * 2^{b, b+1, b+2}.
+__host__ __device__ __forceinline__ void tri_words(uint32_t pa, uint32_t pb, uint32_t pc,
+                                                   uint32_t w[2])
+{
+    w[0] = (pa << 8) | (pb << 16) | ((pa ^ pb) << 24);
+    w[1] = w[0] ^ (pc * 0x01010101u);
+}
+
+__host__ __device__ inline MulTable make_mul_table(uint32_t c)
+{
+    uint32_t p[8];  // c * 2^i
+    p[0] = c & 0xffu;
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+        p[i] = mul2_byte(p[i - 1]);
+    MulTable t;
+    tri_words(p[0], p[1], p[2], t.t0);
+    tri_words(p[3], p[4], p[5], t.t1);
+    t.t2 = (p[6] << 8) | (p[7] << 16) | ((p[6] ^ p[7]) << 24);
+    return t;
+}
+
+__device__ __forceinline__ uint32_t gf_mulc(const MulTable& t, uint32_t x)
+{
+    const uint32_t s0 = x & 0x07070707u;
+    const uint32_t s1 = (x >> 3) & 0x07070707u;
+    const uint32_t s2 = (x >> 6) & 0x03030303u;
+    return __builtin_amdgcn_perm(t.t0[1], t.t0[0], s0) ^
+           __builtin_amdgcn_perm(t.t1[1], t.t1[0], s1) ^ __builtin_amdgcn_perm(0u, t.t2, s2);
+}
+__device__ __forceinline__ u32x4 gf_mulc(const MulTable& t, u32x4 x)
 {
     u32x4 r;
     r.x = gf_mulc(t, x.x);

@@ -278,6 +278,19 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
         return draid::fail_arg("host reconstruct needs k + m <= 255");
     const uint32_t k = h->k, m = h->m, n = k + m;
     const uint64_t S = h->strip_len;
+    // The table is host memory here, so stripes that cannot be rebuilt are found
+    // before anything runs (raid5_simple fails the stripe on an arithmetic error,
+    // raid5_simple.c:177-180,321-325; a storage engine must not report success
+    // for strips it left as they were).
+    for (uint32_t s = 0; s < h->nstripes; ++s) {
+        const uint8_t* f = fail + 2 * static_cast<size_t>(s);
+        const bool oob = (f[0] != DRAID_EC_FAIL_NONE && f[0] >= n) ||
+                         (f[1] != DRAID_EC_FAIL_NONE && f[1] >= n);
+        const uint32_t nf = (f[0] < n ? 1u : 0u) + ((f[1] < n && f[1] != f[0]) ? 1u : 0u);
+        if (oob || nf > m)
+            return draid::fail_arg("host reconstruct: a stripe lists more failures than m or an "
+                                   "index outside the stripe (nothing was rebuilt)");
+    }
     if (!(h->flags & DRAID_EC_HOST_STAGED))
         if (uint8_t* d = mapped_range(h->base, host_span(h)))
             return run_mapped([&](HostEngine& eng, hipStream_t st) {
@@ -297,7 +310,7 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
                     return e;
                 return draid::launch_reconstruct_strided(k, m, S, h->nstripes, d,
                                                          h->strip_stride, h->stripe_stride,
-                                                         eng.zfail, st);
+                                                         eng.zfail, nullptr, st);
             });
     return run_chunks(
         h, chunk_stripes, 0, n,
@@ -308,7 +321,7 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
                 return e;
             return draid::launch_reconstruct(k, m, S, rows,
                                              reinterpret_cast<const uint8_t* const*>(s.table),
-                                             nullptr, s.fail, 0xff, 0xff, s.stream);
+                                             nullptr, s.fail, 0xff, 0xff, nullptr, s.stream);
         },
         [&](Stage& s, uint32_t c0, uint32_t rows, uint8_t* hb) {
             for (uint32_t r = 0; r < rows; ++r) {

@@ -233,10 +233,19 @@ __device__ __forceinline__ bool stripe_aligned(const Ptrs& pp, uint32_t s, int k
 //         2: persistent grid-stride over stripe-major items
 //   PLAN  (reconstruct) 0: exp/log tables staged in LDS, 1: scalar reads of
 //         the __constant__ tables (no LDS, no barrier)
-template <int NTHR_, int U_, int POL_, int MAP_, int PLAN_ = 0>
+//   WAVES waves per SIMD the kernel is built for (0: the compiler's choice).
+//         The compiler pads the register allocation so exactly this many waves
+//         fit: fewer resident waves keep fewer DRAM pages open at once, which
+//         is worth more to these streaming kernels than the extra latency
+//         hiding (8+2 x 64 KiB dual reconstruct: 0.411 ms at 5 waves, 0.420 at
+//         the 7 its 70 VGPRs would allow, 0.417 at 4).
+template <int NTHR_, int U_, int POL_, int MAP_, int PLAN_ = 0, int WAVES_ = 0>
 struct Cfg {
-    static constexpr int NTHR = NTHR_, U = U_, POL = POL_, MAP = MAP_, PLAN = PLAN_;
+    static constexpr int NTHR = NTHR_, U = U_, POL = POL_, MAP = MAP_, PLAN = PLAN_,
+                         WAVES = WAVES_;
 };
+#define DRAID_WAVES_PER_EU(C) \
+    __attribute__((amdgpu_waves_per_eu((C::WAVES) ? (C::WAVES) : 1, (C::WAVES) ? (C::WAVES) : 8)))
 
 template <class C>
 __device__ __forceinline__ void item_coords(uint32_t b, uint32_t cps, uint32_t nstripes,
@@ -303,7 +312,7 @@ __device__ __forceinline__ bool encode_item(const Ptrs& pp, uint32_t s, uint32_t
 }
 
 template <int KT, int M, bool CHECK, class C, class Ptrs>
-__global__ __launch_bounds__(C::NTHR) void k_encode(Ptrs pp, uint32_t k_rt, uint32_t len,
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode(Ptrs pp, uint32_t k_rt, uint32_t len,
                                                     uint32_t cps, uint32_t nstripes,
                                                     uint32_t* flag)
 {
@@ -330,7 +339,8 @@ struct RecPlan {
     bool lostP, lostQ; // parity strips to regenerate
     bool needq;        // the Q syndrome over the survivors is needed
     bool skip;         // unrecoverable / nothing to do
-    NibTable t1, t2;   // constant multipliers (see plan_constants)
+    bool bad;          // more failures than M parities, or an index outside the stripe
+    MulTable t1, t2;   // constant multipliers (see plan_constants)
 };
 
 // Decodes the (wave-uniform) failure pair: which strips are lost, which
@@ -344,13 +354,18 @@ __device__ __forceinline__ RecPlan decode_failures(int k, uint32_t f0, uint32_t 
     pl.nd = 0;
     pl.lostP = false;
     pl.lostQ = false;
+    bool oob = false;
     const uint32_t f[2] = {static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(f0)),
                            static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(f1))};
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
         const int j = static_cast<int>(f[t]);
-        if (f[t] == 0xffu || j >= k + M)
+        if (f[t] == 0xffu)
             continue;
+        if (j >= k + M) {
+            oob = true;
+            continue;
+        }
         if (j < k) {
             if (pl.nd == 1 && pl.x == j)
                 continue;
@@ -372,6 +387,7 @@ __device__ __forceinline__ RecPlan decode_failures(int k, uint32_t f0, uint32_t 
     }
     const int nf = pl.nd + (pl.lostP ? 1 : 0) + (pl.lostQ ? 1 : 0);
     pl.skip = (nf == 0) || (nf > M);
+    pl.bad = oob || nf > M;
     pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
     return pl;
 }
@@ -395,14 +411,18 @@ __device__ __forceinline__ void plan_constants(RecPlan& pl, const uint8_t* t_exp
     // Wave-uniform (one stripe per workgroup): the table build runs on the SALU.
     c1 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c1));
     c2 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c2));
-    pl.t1 = make_nib_table(c1);
-    pl.t2 = make_nib_table(c2);
+    pl.t1 = make_mul_table(c1);
+    pl.t2 = make_mul_table(c2);
 }
 
 // Loads and syndrome accumulation for U elements, then `constants(pl)` (which
 // may stage tables and hit a workgroup barrier -- every lane calls it exactly
 // once, after its loads are in flight), then the outputs.
-template <int KT, int M, int U, int POL, bool BOUNDED, bool NOMUL, class W, class Ptrs, class F>
+// QS == false: the plan needs no Q syndrome (one data strip rebuilt from P, or P
+// alone regenerated), so the Horner doublings -- most of the kernel's VALU work --
+// are not compiled into this instance at all.
+template <int KT, int M, int U, int POL, bool BOUNDED, bool NOMUL, bool QS, class W, class Ptrs,
+          class F>
 __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k, RecPlan& pl,
                                               uint32_t i0, uint32_t stride, uint32_t n,
                                               F&& constants)
@@ -437,7 +457,7 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             ps[u] ^= d[u];
-            if constexpr (M == 2)
+            if constexpr (M == 2 && QS)
                 qs[u] = gf_mul2(qs[u]) ^ d[u];
         }
     });
@@ -531,33 +551,38 @@ __device__ __forceinline__ void reconstruct_item(const Ptrs& pp, uint32_t s, uin
     if (stripe_aligned<KT, M>(pp, s, k)) {
         const uint32_t i0 = c * EPB + threadIdx.x;
         if ((c + 1) * EPB <= nvec) {
-            recover_elems<KT, M, U, POL, false, C::PLAN == 3, u32x4>(pp, s, k, pl, i0, NTHR, nvec,
-                                                                      constants);
+            if (M == 2 && !pl.needq)  // wave-uniform
+                recover_elems<KT, M, U, POL, false, C::PLAN == 3, false, u32x4>(
+                    pp, s, k, pl, i0, NTHR, nvec, constants);
+            else
+                recover_elems<KT, M, U, POL, false, C::PLAN == 3, true, u32x4>(
+                    pp, s, k, pl, i0, NTHR, nvec, constants);
         } else {
             // Partial last chunk (rare): one vector at a time keeps this path's
             // registers below the main path's, so it does not cap occupancy.
             constants(pl);
 #pragma unroll 1
             for (int u = 0; u < U; ++u)
-                recover_elems<KT, M, 1, POL, true, false, u32x4>(pp, s, k, pl, i0 + u * NTHR, NTHR, nvec,
+                recover_elems<KT, M, 1, POL, true, false, true, u32x4>(pp, s, k, pl, i0 + u * NTHR, NTHR, nvec,
                                                           none);
         }
         const uint32_t tail = len & 15u;
         if (tail && c == cps - 1 && threadIdx.x < tail)
-            recover_elems<0, M, 1, 0, true, false, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
                                                       NTHR, len, none);
     } else {
         constants(pl);
         const uint32_t b1 = min(len, (c + 1) * EPB * 16);
         for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += NTHR)
-            recover_elems<0, M, 1, 0, true, false, uint32_t>(pp, s, k, pl, b, NTHR, b1, none);
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, k, pl, b, NTHR, b1, none);
     }
 }
 
 template <int KT, int M, class C, class Ptrs>
-__global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt, uint32_t len,
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(Ptrs pp, uint32_t k_rt, uint32_t len,
                                                          uint32_t cps, uint32_t nstripes,
-                                                         const uint8_t* fail, uint32_t f01)
+                                                         const uint8_t* fail, uint32_t f01,
+                                                         uint32_t* bad)
 {
     __shared__ LdsGf lds;
     const uint8_t* l_exp = reinterpret_cast<const uint8_t*>(lds.w);
@@ -578,14 +603,18 @@ __global__ __launch_bounds__(C::NTHR) void k_reconstruct(Ptrs pp, uint32_t k_rt,
             f1 = fail[2 * (size_t)s + 1];
         }
         RecPlan pl = decode_failures<M>(k, f0, f1);
+        // A stripe that cannot be rebuilt is left untouched and counted once (by
+        // the workgroup of its first chunk) when the caller asked for the count.
+        if (bad && pl.bad && c == 0 && threadIdx.x == 0)
+            atomicAdd(bad, 1u);
         if (pl.skip)
             continue;  // uniform across the workgroup
         if constexpr (C::PLAN == 2 || C::PLAN == 3) {
             // DIAGNOSTIC ONLY (tools/sweep.py): constants left zero, no LDS, no
             // barrier -- wrong results, measures what the plan step costs.
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-                p.t1 = make_nib_table(0);
-                p.t2 = make_nib_table(0);
+                p.t1 = make_mul_table(0);
+                p.t2 = make_mul_table(0);
             });
         } else if constexpr (C::PLAN == 1) {
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
@@ -642,7 +671,7 @@ struct WorkSrc {
 };
 
 template <int KT, int M, bool CHECK, class C>
-__global__ __launch_bounds__(C::NTHR) void k_encode_work(TablePtrs pp, uint32_t k_rt, WorkSrc ws,
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(TablePtrs pp, uint32_t k_rt, WorkSrc ws,
                                                          uint32_t nwork)
 {
     constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
@@ -655,7 +684,7 @@ __global__ __launch_bounds__(C::NTHR) void k_encode_work(TablePtrs pp, uint32_t 
 }
 
 template <int KT, int M, class C>
-__global__ __launch_bounds__(C::NTHR) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
                                                               WorkSrc ws, const uint8_t* fail,
                                                               uint32_t fstride, uint32_t nwork)
 {
@@ -834,7 +863,7 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
 
 template <int KT, int M, class C, class Ptrs>
 static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
-                                 const uint8_t* fail, uint32_t f01, hipStream_t st)
+                                 const uint8_t* fail, uint32_t f01, uint32_t* bad, hipStream_t st)
 {
     uint32_t cps, grid;
     if (nstripes == 0 || len == 0)
@@ -842,7 +871,7 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
     if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp, k,
-                       static_cast<uint32_t>(len), cps, nstripes, fail, f01);
+                       static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
     return hipGetLastError();
 }
 
@@ -869,15 +898,42 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
 // (6496 vs 6500), 128 KiB +0.8%, 16+2 +0.3%, 4+1 -0.4%.  Buffer loads in the
 // reconstruct lose 1.8% at 8+2 x 64 KiB (they win 1-2% at 128/256 KiB).
 constexpr int kLanes = 64;
-template <int U, int MAP = 0>
-using EncCfg = Cfg<kLanes, U, pol_aux(2, 18), MAP, 0>;
+// Waves per SIMD each kernel is built for (Cfg::WAVES), from a sweep of every
+// setting over the stripe shapes (tools/gpu_shape_matrix.sh, same-box A/B of whole
+// library builds, profiles/r02/occupancy/): the best count falls as a wave's
+// loads in flight grow with k.  Microseconds per 4096-stripe launch, best vs the
+// compiler's own choice:
+//   encode       8+2 x 64 KiB 403.8 vs 411.5 (6 waves), 8+2 x 128 KiB 804.7 vs 850.7,
+//                10+2 498.8 vs 508.1, 16+2 x 256 KiB 402.4 vs 410.2, 4+1 203.7 vs 205.2 (7)
+//   reconstruct  8+2 x 64 KiB dual 411 vs 420 (5; 4 -> 417), 8+2 x 128 KiB 822.8 vs 858.0
+//                (4; 5 -> 837.6), 10+2 498.3 vs 509.4 (4), 16+2 x 256 KiB 399.2 vs 408.6 (3),
+//                4+1 and 6+2: the compiler's choice (7-8 waves) is already best.
+// DRAID_ENC_WAVES / DRAID_REC_WAVES (>= 0) override every k, for such sweeps only.
+#ifndef DRAID_ENC_WAVES
+#define DRAID_ENC_WAVES -1
+#endif
+#ifndef DRAID_REC_WAVES
+#define DRAID_REC_WAVES -1
+#endif
+constexpr uint64_t kBigStrip = 128u << 10;  // strips from here on use the *_big counts
+constexpr int enc_waves(int k) { return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES : k <= 4 ? 7 : 6; }
+constexpr int rec_waves(int k)
+{
+    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES : k <= 6 ? 0 : k <= 8 ? 5 : k <= 12 ? 4 : 3;
+}
+constexpr int rec_waves_big(int k)
+{
+    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES : (k == 7 || k == 8) ? 4 : rec_waves(k);
+}
+template <int U, int MAP = 0, int WAVES = 0>
+using EncCfg = Cfg<kLanes, U, pol_aux(2, 18), MAP, 0, WAVES>;
 // Item order of the batched encode: XCD-aware (each XCD a contiguous run of
 // stripes) from k = 16 up -- 16+2 x 256 KiB encode 5988 vs 5747 GB/s (+4.2%,
 // lab variant 38 vs 0, median of 5 rounds, profiles/r01/cachepol/xcd_*.json) -- while it
 // costs 2-3% at 4+1 / 8+2 x 64 and 128 KiB, so the smaller k keep stripe order.
 constexpr int enc_map(int k) { return k >= 16 ? 3 : 0; }
-template <int U>
-using RecCfg = Cfg<kLanes, U, pol_aux(-1, 18), 0, 0>;
+template <int U, int WAVES = 0>
+using RecCfg = Cfg<kLanes, U, pol_aux(-1, 18), 0, 0, WAVES>;
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 
@@ -891,8 +947,8 @@ static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint
     switch (k) {
 #define DRAID_CASE(K) \
     case K:           \
-        return go_encode<K, M, false, EncCfg<enc_unroll(K), enc_map(K)>>(pp, k, len, nstripes,  \
-                                                                        nullptr, st);
+        return go_encode<K, M, false, EncCfg<enc_unroll(K), enc_map(K), enc_waves(K)>>(         \
+            pp, k, len, nstripes, nullptr, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
@@ -903,17 +959,20 @@ static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint
 template <int M, class Ptrs>
 static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
                                        uint32_t nstripes, const uint8_t* fail, uint32_t f01,
-                                       hipStream_t st)
+                                       uint32_t* bad, hipStream_t st)
 {
     switch (k) {
 #define DRAID_CASE(K)                                                                       \
     case K:                                                                                 \
-        return go_reconstruct<K, M, RecCfg<rec_unroll(K)>>(pp, k, len, nstripes, fail, \
-                                                               f01, st);
+        return len >= kBigStrip                                                             \
+                   ? go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_waves_big(K)>>(         \
+                         pp, k, len, nstripes, fail, f01, bad, st)                          \
+                   : go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_waves(K)>>(             \
+                         pp, k, len, nstripes, fail, f01, bad, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return go_reconstruct<0, M, RecCfg<2>>(pp, k, len, nstripes, fail, f01, st);
+        return go_reconstruct<0, M, RecCfg<2>>(pp, k, len, nstripes, fail, f01, bad, st);
     }
 }
 
@@ -996,11 +1055,11 @@ static hipError_t variant_reconstruct(int v, const TablePtrs& pp, uint64_t len, 
     switch (v) {
 #define DRAID_V(N, C) \
     case N:           \
-        return go_reconstruct<K, M, C>(pp, K, len, ns, fail, 0xffffu, st);
+        return go_reconstruct<K, M, C>(pp, K, len, ns, fail, 0xffffu, nullptr, st);
         DRAID_VARIANTS(DRAID_V)
 #undef DRAID_V
     default:
-        return go_reconstruct<K, M, RecCfg<rec_unroll(K)>>(pp, K, len, ns, fail, 0xffffu, st);
+        return go_reconstruct<K, M, RecCfg<rec_unroll(K)>>(pp, K, len, ns, fail, 0xffffu, nullptr, st);
     }
 }
 
@@ -1035,7 +1094,8 @@ hipError_t launch_encode(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes
 
 hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
                               const uint8_t* const* table, const ArgPtrTable* args,
-                              const uint8_t* fail_dev, uint8_t f0, uint8_t f1, hipStream_t st)
+                              const uint8_t* fail_dev, uint8_t f0, uint8_t f1, uint32_t* bad,
+                              hipStream_t st)
 {
     const uint32_t f01 = static_cast<uint32_t>(f0) | (static_cast<uint32_t>(f1) << 8);
     if (table) {
@@ -1049,13 +1109,13 @@ hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nst
                           : variant_reconstruct<16, 2>(v, pp, len, nstripes, fail_dev, st);
 #endif
         if (m == 1)
-            return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, f01, st);
-        return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, f01, st);
+            return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, f01, bad, st);
+        return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, f01, bad, st);
     }
     const ArgPtrs pp{*args};
     if (m == 1)
-        return dispatch_reconstruct<1>(pp, k, len, 1, fail_dev, f01, st);
-    return dispatch_reconstruct<2>(pp, k, len, 1, fail_dev, f01, st);
+        return dispatch_reconstruct<1>(pp, k, len, 1, fail_dev, f01, bad, st);
+    return dispatch_reconstruct<2>(pp, k, len, 1, fail_dev, f01, bad, st);
 }
 
 hipError_t launch_encode_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
@@ -1071,12 +1131,12 @@ hipError_t launch_encode_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t 
 hipError_t launch_reconstruct_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
                                       const uint8_t* base, uint64_t strip_stride,
                                       uint64_t stripe_stride, const uint8_t* fail_dev,
-                                      hipStream_t st)
+                                      uint32_t* bad, hipStream_t st)
 {
     const StridedPtrs pp{base, strip_stride, stripe_stride};
     if (m == 1)
-        return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, 0xffff, st);
-    return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, 0xffff, st);
+        return dispatch_reconstruct<1>(pp, k, len, nstripes, fail_dev, 0xffff, bad, st);
+    return dispatch_reconstruct<2>(pp, k, len, nstripes, fail_dev, 0xffff, bad, st);
 }
 
 hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* const* table,
@@ -1156,10 +1216,10 @@ hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* tabl
     switch (k) {
 #define DRAID_CASE(K)                                                                        \
     case K:                                                                                  \
-        return m == 1 ? go_encode_work<K, 1, EncCfg<enc_unroll(K)>>(table, k, seg_len,   \
-                                                                        work, ulen, nwork, st) \
-                      : go_encode_work<K, 2, EncCfg<enc_unroll(K)>>(table, k, seg_len,   \
-                                                                        work, ulen, nwork, st);
+        return m == 1 ? go_encode_work<K, 1, EncCfg<enc_unroll(K), 0, enc_waves(K)>>(        \
+                            table, k, seg_len, work, ulen, nwork, st)                        \
+                      : go_encode_work<K, 2, EncCfg<enc_unroll(K), 0, enc_waves(K)>>(        \
+                            table, k, seg_len, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
@@ -1177,9 +1237,9 @@ hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const*
     switch (k) {
 #define DRAID_CASE(K)                                                                         \
     case K:                                                                                   \
-        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K)>>(                 \
+        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K), rec_waves(K)>>(       \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st) \
-                      : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K)>>(                 \
+                      : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K), rec_waves(K)>>(       \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE

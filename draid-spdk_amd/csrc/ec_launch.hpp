@@ -40,13 +40,15 @@ hipError_t launch_encode_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t 
 hipError_t launch_reconstruct_strided(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
                                       const uint8_t* base, uint64_t strip_stride,
                                       uint64_t stripe_stride, const uint8_t* fail_dev,
-                                      hipStream_t stream);
+                                      uint32_t* bad_dev, hipStream_t stream);
 
 // Reconstruct.  fail_dev: device [nstripes][2] (0xFF = none); when null,
-// (f0, f1) apply to every stripe.
+// (f0, f1) apply to every stripe.  bad_dev (may be null): device-accessible
+// counter incremented once per stripe that cannot be rebuilt (more failures
+// than m, or an index outside the stripe).
 hipError_t launch_reconstruct(uint32_t k, uint32_t m, uint64_t len, uint32_t nstripes,
                               const uint8_t* const* table, const ArgPtrTable* args,
-                              const uint8_t* fail_dev, uint8_t f0, uint8_t f1,
+                              const uint8_t* fail_dev, uint8_t f0, uint8_t f1, uint32_t* bad_dev,
                               hipStream_t stream);
 
 // Check: sets *flag_dev to non-zero if any stored parity differs.
@@ -85,6 +87,14 @@ hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* tab
 // message for draid_ec_last_error(); fail_hip returns -hipError, fail_arg 1.
 int fail_hip(hipError_t e, const char* what);
 int fail_arg(const char* what);
+
+// Pointer resolution (ec_xlate.cpp): the address a kernel may use for the
+// caller's [p, p + len) -- device memory as is, pinned / registered host memory
+// at its device address.  Returns 0, or 1 when the range is not GPU accessible
+// (pageable host memory): such a pointer must never reach a kernel.  Results are
+// cached per thread; translate_invalidate() empties every thread's cache.
+int translate(const void* p, size_t len, const void** dev);
+void translate_invalidate();
 
 // Variant selector for A/B experiments inside one process (0 = default).
 void set_variant(int v);

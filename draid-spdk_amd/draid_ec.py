@@ -36,7 +36,10 @@ EXPORTS = (
     "draid_ec_ctx_queued", "draid_ec_host_encode", "draid_ec_host_reconstruct",
     "draid_ec_encode_strided", "draid_ec_reconstruct_strided",
     "draid_ec_ctx_update_sg", "draid_ec_host_device_pointer", "draid_ec_ctx_set_autoflush",
-    "draid_pq_check_static",
+    "draid_pq_check_static", "draid_ec_reconstruct_status",
+    "draid_ec_reconstruct_strided_status", "draid_ec_device_pointer",
+    "draid_ec_pointer_cache_flush", "draid_ec_ctx_flush_ticket", "draid_ec_ctx_ticket_query",
+    "draid_ec_ctx_set_host_pointers",
 )
 
 
@@ -97,6 +100,10 @@ def lib() -> C.CDLL:
         L.draid_recover.argtypes = [i32, i32, i32, C.POINTER(vp), i32, C.POINTER(i32)]
         L.draid_ec_encode.argtypes = [C.POINTER(StripeBatch), vp]
         L.draid_ec_reconstruct.argtypes = [C.POINTER(StripeBatch), vp, vp]
+        L.draid_ec_reconstruct_status.argtypes = [C.POINTER(StripeBatch), vp, vp, vp]
+        L.draid_ec_reconstruct_strided_status.argtypes = [C.POINTER(HostStripes), vp, vp, vp]
+        L.draid_ec_device_pointer.argtypes = [vp, C.c_size_t, C.POINTER(vp)]
+        L.draid_ec_pointer_cache_flush.restype = None
         L.draid_ec_last_error.restype = C.c_char_p
         L.draid_ec_set_device.argtypes = [i32]
         L.draid_ec_device_count.argtypes = [C.POINTER(i32)]
@@ -119,6 +126,11 @@ def lib() -> C.CDLL:
         L.draid_ec_ctx_queued.argtypes = [vp]
         L.draid_ec_ctx_queued.restype = C.c_uint64
         L.draid_ec_ctx_set_autoflush.argtypes = [vp, C.c_uint64]
+        L.draid_ec_ctx_flush_ticket.argtypes = [vp, C.POINTER(C.c_uint64)]
+        L.draid_ec_ctx_ticket_query.argtypes = [vp, C.c_uint64]
+        L.draid_ec_ctx_set_host_pointers.argtypes = [vp, i32]
+        L.draid_ec_ctx_test_fail_after.argtypes = [vp, i32]
+        L.draid_ec_ctx_test_fail_after.restype = None
         L.draid_ec_ctx_encode_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t]
         L.draid_ec_ctx_reconstruct_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp,
                                                   C.c_size_t, i32, vp]
@@ -213,6 +225,19 @@ def reconstruct(batch: StripeBatch, fail_ptr, stream: int) -> int:
                   "ec_reconstruct")
 
 
+def reconstruct_status(batch: StripeBatch, fail_ptr, counter_ptr, stream: int) -> int:
+    return _check(lib().draid_ec_reconstruct_status(C.byref(batch), _ptr(fail_ptr),
+                                                    _ptr(counter_ptr), stream),
+                  "ec_reconstruct_status")
+
+
+def device_pointer(ptr: int, nbytes: int):
+    """Address a kernel may use for [ptr, ptr + nbytes), or None (pageable host memory)."""
+    d = C.c_void_p()
+    rc = _check(lib().draid_ec_device_pointer(ptr, nbytes, C.byref(d)), "device_pointer")
+    return None if rc else d.value
+
+
 def stream_create() -> int:
     s = C.c_void_p()
     _check(lib().draid_ec_stream_create(C.byref(s)), "stream_create")
@@ -257,8 +282,12 @@ def encode_strided(base, k, m, strip_len, nstripes, strip_stride, stripe_stride,
 
 
 def reconstruct_strided(base, k, m, strip_len, nstripes, strip_stride, stripe_stride, fail,
-                        stream: int) -> int:
+                        stream: int, counter=None) -> int:
     d = HostStripes(k, m, strip_len, nstripes, 0, _ptr(base), strip_stride, stripe_stride)
+    if counter is not None:
+        return _check(lib().draid_ec_reconstruct_strided_status(C.byref(d), _ptr(fail),
+                                                                _ptr(counter), stream),
+                      "reconstruct_strided_status")
     return _check(lib().draid_ec_reconstruct_strided(C.byref(d), _ptr(fail), stream),
                   "reconstruct_strided")
 
@@ -341,6 +370,21 @@ class Ctx:
 
     def queued(self):
         return lib().draid_ec_ctx_queued(self.h)
+
+    def flush_ticket(self) -> int:
+        t = C.c_uint64()
+        _check(lib().draid_ec_ctx_flush_ticket(self.h, C.byref(t)), "ctx_flush_ticket")
+        return t.value
+
+    def ticket_query(self, ticket: int) -> int:
+        return _check(lib().draid_ec_ctx_ticket_query(self.h, ticket), "ctx_ticket_query")
+
+    def set_host_pointers(self, on: bool):
+        return _check(lib().draid_ec_ctx_set_host_pointers(self.h, int(on)), "ctx_set_host_pointers")
+
+    def test_fail_after(self, n: int):
+        """Test hook: the n-th descriptor piece launched from now on fails."""
+        lib().draid_ec_ctx_test_fail_after(self.h, n)
 
     def set_autoflush(self, segments: int):
         return _check(lib().draid_ec_ctx_set_autoflush(self.h, segments), "ctx_set_autoflush")

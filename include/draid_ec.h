@@ -7,12 +7,15 @@
  *
  *  1. The isa-l v2.30 arithmetic ABI the raid modules call (raid.h /
  *     gf_vect_mul.h), re-implemented as HIP kernels on gfx950.  Same argument
- *     meaning, same array order, same 0 / non-zero return convention.  Every
- *     buffer pointer must be device-accessible (hipMalloc'd HBM, or host memory
- *     registered with draid_ec_host_register(), addressed through
- *     draid_ec_host_device_pointer()).  Calls are synchronous, like
- *     isa-l's: they run on the calling thread's per-thread stream and return
- *     once the result is in memory.
+ *     meaning, same array order, same 0 / non-zero return convention, and --
+ *     like isa-l, which the reference hands spdk_dma_malloc'd chunk buffers and
+ *     user iovecs (raid5.c:188-201) -- any kind of pointer: device memory is
+ *     used in place; pinned or registered host memory is read and written in
+ *     place through its device address (looked up per call, cached per thread);
+ *     pageable host memory is copied through a per-thread device staging
+ *     buffer.  No pointer the GPU cannot reach is ever handed to a kernel.
+ *     Calls are synchronous, like isa-l's: they run on the calling thread's
+ *     per-thread stream and return once the result is in memory.
  *
  *  2. A batched, asynchronous stripe API for the GPU path proper: many
  *     independent stripes per launch through a device-resident pointer table,
@@ -135,6 +138,16 @@ int draid_ec_encode(const draid_ec_stripe_batch *batch, void *stream);
 int draid_ec_reconstruct(const draid_ec_stripe_batch *batch, const uint8_t *fail,
                          void *stream);
 
+/* draid_ec_reconstruct that also reports what it could not rebuild (the
+ * reference fails a stripe whose arithmetic fails, raid5_simple.c:177-180,
+ * 321-325): *unrecoverable, a device-accessible uint32_t (device memory, or the
+ * device address of pinned host memory), is incremented once for every stripe
+ * whose pair lists more failures than m or an index in [k+m, 0xFF).  Those
+ * stripes are left untouched.  The counter is only added to: clear it before
+ * the call (or accumulate over several); read it once `stream` has finished. */
+int draid_ec_reconstruct_status(const draid_ec_stripe_batch *batch, const uint8_t *fail,
+                                uint32_t *unrecoverable, void *stream);
+
 /* Regular layout, no pointer table: strip j of stripe s at
  * base + s*stripe_stride + j*strip_stride (a stripe cache allocated as one
  * array, raid5.c:1331-1353 with the n chunk buffers of a stripe adjacent). */
@@ -154,6 +167,8 @@ typedef struct draid_ec_strided_stripes {
 int draid_ec_encode_strided(const draid_ec_strided_stripes *s, void *stream);
 int draid_ec_reconstruct_strided(const draid_ec_strided_stripes *s, const uint8_t *fail,
                                  void *stream);
+int draid_ec_reconstruct_strided_status(const draid_ec_strided_stripes *s, const uint8_t *fail,
+                                        uint32_t *unrecoverable, void *stream);
 
 /* ------------------------------------------------------------------------
  * 2b. Scatter-gather stripes through a per-channel context
@@ -175,7 +190,14 @@ void *draid_ec_ctx_stream(draid_ec_ctx *ctx);
 
 /* Queue one stripe's encode.  Strip j (k data, then P, then Q) is `len` bytes
  * starting `offset[j]` bytes into iovs[j][0 .. iovcnt[j]) (offset may be NULL).
- * Every iov_base must be device-accessible. */
+ * Every iov_base is a device-usable address (device memory, or the device
+ * address of pinned / registered host memory) -- unless the context resolves
+ * host pointers itself, see draid_ec_ctx_set_host_pointers.
+ * The queueing calls (encode_sg, reconstruct_sg, update_sg) normally only write
+ * descriptors into pinned memory.  They can wait -- for the descriptor upload of
+ * the flush before last, when a group is queued into again while those copies
+ * still run -- and they allocate pinned memory when a group outgrows its
+ * descriptor storage (it doubles, from 1 MiB). */
 int draid_ec_ctx_encode_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m,
                            const struct iovec *const *iovs, const int *iovcnt,
                            const size_t *offset, size_t len);
@@ -197,14 +219,40 @@ int draid_ec_ctx_update_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m, uint32_t n
                            const int *new_cnt, const struct iovec *const *par_iovs,
                            const int *par_cnt, size_t len);
 
-/* Launch everything queued (non-blocking; blocks only if the descriptor ring
- * is 4 flushes behind).  The context's stream is non-blocking: it does not wait
- * for work on other streams, so every queued buffer must hold its data when
- * flush is called.  Stripes queued with the same (op, k, m) carry no order
- * among themselves (the flush may run them in address order); groups run in
- * the order they were first queued.  draid_ec_ctx_query: 0 idle, 1 running,
- * < 0 error. */
+/* Launch everything queued.  Non-blocking, except that each ~1 MiB piece of
+ * descriptors takes one of 8 ring slots and waits for that slot's previous
+ * kernel when all 8 are in flight (and allocates the slot's buffers on first
+ * use or growth).  The context's stream is non-blocking: it does not wait for
+ * work on other streams, so every queued buffer must hold its data when flush
+ * is called.
+ * Order: segments queued with the same (op, k, m) form a group and carry no
+ * order among themselves (the flush may run them in address order).  Groups
+ * run in the order in which their FIRST segment of this batch was queued, on
+ * one stream.  So work that depends on an earlier group's output may share a
+ * batch with it (reconstruct into chunk buffers, then an encode reading them)
+ * as long as the earlier group is not queued into again afterwards; any other
+ * dependency needs a flush in between.
+ * On failure (a piece's descriptor memory, the work-item limit, a launch
+ * error) the pieces launched so far keep running, every segment that did not
+ * launch stays queued -- draid_ec_ctx_queued() counts exactly those -- and the
+ * error is returned: flush again, or fail the requests still queued.
+ * draid_ec_ctx_query: 0 idle, 1 running, < 0 error. */
 int draid_ec_ctx_flush(draid_ec_ctx *ctx);
+/* draid_ec_ctx_flush, then a ticket for everything launched so far:
+ * draid_ec_ctx_ticket_query(ticket) is 0 once all of it has finished, 1 while it
+ * runs -- whatever was flushed later may still be running.  This is what a
+ * poller completes requests on (draid_ec_ctx_query only turns 0 when the whole
+ * stream is idle, which a busy channel never is).  At most 64 tickets may be
+ * outstanding; the 65th flush_ticket waits for the oldest. */
+int draid_ec_ctx_flush_ticket(draid_ec_ctx *ctx, uint64_t *ticket);
+int draid_ec_ctx_ticket_query(draid_ec_ctx *ctx, uint64_t ticket);
+/* on != 0: every iov_base handed to this context is the CALLER'S address -- a
+ * host pointer of pinned / registered memory (an SPDK buffer) or a device
+ * pointer -- and is resolved to its device address while the descriptors are
+ * written (draid_ec_device_pointer's cached lookup, one per iovec).  A stripe
+ * with an iovec the GPU cannot reach is rejected with 1 and queues nothing.
+ * Off by default. */
+int draid_ec_ctx_set_host_pointers(draid_ec_ctx *ctx, int on);
 int draid_ec_ctx_query(draid_ec_ctx *ctx);
 int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);
 uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last flush */
@@ -241,7 +289,9 @@ typedef draid_ec_strided_stripes draid_ec_host_stripes;   /* base is HOST memory
 int draid_ec_host_encode(const draid_ec_host_stripes *h, uint32_t chunk_stripes);
 
 /* All k+m strips in, the failed strips (HOST fail[nstripes][2], as
- * draid_ec_reconstruct) out. */
+ * draid_ec_reconstruct) out.  The table is checked before anything runs: a
+ * stripe with more failures than m, or an index in [k+m, 0xFF), -> 1 and nothing
+ * is rebuilt. */
 int draid_ec_host_reconstruct(const draid_ec_host_stripes *h, const uint8_t *fail,
                               uint32_t chunk_stripes);
 
@@ -273,6 +323,16 @@ int draid_ec_host_unregister(void *ptr);
  * 2c calls take host addresses and translate themselves.  Returns 0, or 1 with
  * *dev_ptr = NULL when ptr is not in a mapped host range. */
 int draid_ec_host_device_pointer(const void *ptr, void **dev_ptr);
+/* The address a kernel may use for the caller's [ptr, ptr + len): device memory
+ * -> itself, pinned / registered host memory -> its device address.  Returns 0,
+ * or 1 with *dev_ptr = NULL when the range is neither (pageable host memory).
+ * This is the lookup every pointer-taking entry point of sections 1 and 2b
+ * does; results are cached per thread by allocation, so a hit costs a few
+ * compares.  The cache is emptied by draid_ec_device_free, draid_ec_host_unregister
+ * and draid_ec_pointer_cache_flush -- call the last one after freeing or
+ * unregistering memory behind the library's back if its addresses may be reused. */
+int draid_ec_device_pointer(const void *ptr, size_t len, void **dev_ptr);
+void draid_ec_pointer_cache_flush(void);
 /* kind: 0 host->device, 1 device->host, 2 device->device. */
 int draid_ec_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *stream);
 

@@ -118,7 +118,22 @@ def test_registered_host_memory(ec):
     assert ec.host_device_pointer(base) is None  # not registered yet
     rng = np.random.default_rng(5)
     buf[:k * L] = rng.integers(0, 256, k * L, dtype=np.uint8)
-    ec.host_register(base, n * L + 4096)
+    try:
+        ec.host_register(base, n * L + 4096)
+    except ec.DraidError as err:
+        # Some boxes' drivers refuse hipHostRegister for every kind of user memory
+        # (shared or private mappings, touched or not, any flag: the plain C probe
+        # tools/probe/host_register_probe.c shows "invalid argument" for all of
+        # them).  Registration is then unavailable to any program on the box, and
+        # only memory from the pinned allocator can be mapped (covered above).
+        probe = mmap.mmap(-1, 1 << 16, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        probe[:] = b"\x01" * (1 << 16)
+        paddr = ctypes.addressof(ctypes.c_char.from_buffer(probe))
+        rc = ec.lib().draid_ec_host_register(paddr, 1 << 16)
+        if rc == 0:
+            ec.host_unregister(paddr)
+            raise  # the box registers memory: the failure above is ours
+        pytest.skip(f"hipHostRegister is refused for any host memory on this box ({err})")
     try:
         dev = ec.host_device_pointer(base)
         assert dev is not None
