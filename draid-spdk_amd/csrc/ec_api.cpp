@@ -478,6 +478,14 @@ int draid_ec_set_device(int device)
     return e == hipSuccess ? 0 : fail_hip(e, "hipSetDevice");
 }
 
+int draid_ec_device_current(int* device)
+{
+    if (!device)
+        return fail_arg("device_current: device is NULL");
+    hipError_t e = hipGetDevice(device);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipGetDevice");
+}
+
 int draid_ec_device_count(int* count)
 {
     if (!count)
@@ -533,6 +541,22 @@ int draid_ec_device_free(void* ptr)
     draid::translate_invalidate();  // cached ranges may name this memory
     hipError_t e = hipFree(ptr);
     return e == hipSuccess ? 0 : fail_hip(e, "hipFree");
+}
+
+int draid_ec_host_alloc(void** ptr, size_t bytes)
+{
+    if (!ptr)
+        return fail_arg("host_alloc: ptr is NULL");
+    *ptr = nullptr;
+    hipError_t e = hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipHostMalloc");
+}
+
+int draid_ec_host_free(void* ptr)
+{
+    draid::translate_invalidate();  // cached ranges may name this memory
+    hipError_t e = hipHostFree(ptr);
+    return e == hipSuccess ? 0 : fail_hip(e, "hipHostFree");
 }
 
 int draid_ec_host_register(void* ptr, size_t bytes)

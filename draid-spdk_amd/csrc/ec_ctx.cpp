@@ -873,6 +873,21 @@ int draid_ec_ctx_synchronize(draid_ec_ctx* c)
 
 uint64_t draid_ec_ctx_queued(draid_ec_ctx* c) { return c ? c->queued_segments : 0; }
 
+int draid_ec_ctx_discard_queued(draid_ec_ctx* c)
+{
+    if (!c)
+        return ctx_arg("ctx is NULL");
+    for (Group& g : c->groups) {
+        if (g.ready())  // the storage may still feed an earlier flush's copies
+            (void)hipStreamSynchronize(c->copy);
+        g.ptrs.clear();
+        g.len.clear();
+        g.fail.clear();
+    }
+    c->queued_segments = 0;
+    return 0;
+}
+
 int draid_ec_ctx_set_autoflush(draid_ec_ctx* c, uint64_t segments)
 {
     if (!c)

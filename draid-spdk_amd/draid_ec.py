@@ -39,7 +39,8 @@ EXPORTS = (
     "draid_pq_check_static", "draid_ec_reconstruct_status",
     "draid_ec_reconstruct_strided_status", "draid_ec_device_pointer",
     "draid_ec_pointer_cache_flush", "draid_ec_ctx_flush_ticket", "draid_ec_ctx_ticket_query",
-    "draid_ec_ctx_set_host_pointers",
+    "draid_ec_ctx_set_host_pointers", "draid_ec_host_alloc", "draid_ec_host_free",
+    "draid_ec_ctx_discard_queued", "draid_ec_device_current",
 )
 
 
@@ -107,6 +108,7 @@ def lib() -> C.CDLL:
         L.draid_ec_last_error.restype = C.c_char_p
         L.draid_ec_set_device.argtypes = [i32]
         L.draid_ec_device_count.argtypes = [C.POINTER(i32)]
+        L.draid_ec_device_current.argtypes = [C.POINTER(i32)]
         L.draid_ec_stream_create.argtypes = [C.POINTER(vp)]
         for f in ("draid_ec_stream_destroy", "draid_ec_stream_query",
                   "draid_ec_stream_synchronize", "draid_ec_device_free",
@@ -114,6 +116,9 @@ def lib() -> C.CDLL:
             getattr(L, f).argtypes = [vp]
         L.draid_ec_device_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
         L.draid_ec_host_register.argtypes = [vp, C.c_size_t]
+        L.draid_ec_host_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
+        L.draid_ec_host_free.argtypes = [vp]
+        L.draid_ec_ctx_discard_queued.argtypes = [vp]
         L.draid_ec_host_device_pointer.argtypes = [vp, C.POINTER(vp)]
         L.draid_ec_memcpy_async.argtypes = [vp, vp, C.c_size_t, i32, vp]
         L.draid_ec_set_variant.argtypes = [i32]

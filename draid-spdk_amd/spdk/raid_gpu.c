@@ -1,0 +1,943 @@
+/*
+ * raid_gpu.c -- RAID6 (and RAID5) level module for SPDK's raid bdev whose parity
+ * arithmetic runs on an MI355X through libdraid_ec.so.
+ *
+ * It plugs into the reference's raid framework exactly as its own level modules
+ * do: a `struct raid_bdev_module` registered with RAID_MODULE_REGISTER
+ * (module/bdev/raid/bdev_raid.h:286-348), called through
+ * raid_bdev_submit_request (bdev_raid.c:495-529) and completing parent I/O with
+ * raid_bdev_io_complete (bdev_raid.c:325-331).  The reference has no RAID6
+ * module: raid6.c is a clone of raid5.c that computes no Q and registers as
+ * RAID5 (raid6.c:189,220,1361-1372).  What each part follows:
+ *
+ *   start / geometry         raid5_start, raid5.c:1399-1489 (draid_raid_start)
+ *   request mapping          raid5_submit_rw_request / raid5_handle_stripe,
+ *                            raid5.c:1292-1324,962-1055 (draid_raid_map_request)
+ *   one request per stripe   the stripe's request queue, raid5.c:1047-1054,485-521
+ *                            (draid_stripe_cache)
+ *   full-stripe write        raid5_stripe_write_preread_complete, raid5.c:743-777,
+ *                            and raid5_xor_stripe, raid5_simple.c:141-203
+ *   partial write            raid5_stripe_write (the RMW / RCW vote) and the two
+ *                            preread-complete handlers, raid5.c:705-867
+ *   read / degraded read     raid5_stripe_read, raid5.c:869-946, and
+ *                            raid5_complete_reconstructed_stripe_request, :544-594
+ *   base bdev I/O, -ENOMEM   raid5_submit_chunk_request, raid5.c:617-689
+ *   per-channel resources    raid5_io_channel_resource_init, raid5.c:1491-1541
+ *
+ * Where the reference calls isa-l synchronously on the reactor, this module
+ * queues the stripe's parity work on a per-channel draid_ec_ctx and returns; a
+ * poller flushes what the reactor iteration queued as ONE launch and finishes
+ * the requests of each flush when its ticket completes.  A reactor never waits
+ * for the GPU.
+ *
+ * Degraded operation (bdev_raid.h:91-92,163; the reference only has the flags
+ * and a commented-out setter, bdev_raid.c:1157-1170): requests read the
+ * per-disk `degraded` flags at submit time.  Up to base_bdevs_max_degraded
+ * disks may be degraded: reads rebuild the lost requested ranges, writes keep
+ * parity consistent and skip the lost disks.  A base bdev I/O error marks the
+ * disk degraded (raid_gpu_set_degraded) and the request is redone against the
+ * new state instead of failing, as long as the array can still tolerate it.
+ *
+ * Buffers: every buffer a kernel touches -- the parent I/O's iovecs and this
+ * module's strip buffers from spdk_dma_malloc -- must be memory the GPU can reach
+ * (SPDK's DMA memory registered once with draid_ec_host_register, or allocated
+ * through draid_ec_host_alloc).  The contexts resolve the host addresses
+ * themselves; an I/O whose buffer is not reachable fails with an error log, it
+ * is never handed to a kernel.
+ */
+#include "bdev_raid.h"
+
+#include "spdk/env.h"
+#include "spdk/likely.h"
+#include "spdk/log.h"
+#include "spdk/string.h"
+#include "spdk/thread.h"
+#include "spdk/util.h"
+
+#include "draid_ec.h"
+#include "draid_raid.h"
+#include "raid_gpu.h"
+
+/* Stripe requests in flight per channel (raid5_simple.c:14 keeps 128 with one
+ * parity buffer each; here each owns n strip buffers). */
+#define RG_MAX_REQUESTS 64
+#define RG_MAX_GPUS 8
+#define RG_CACHE_STRIPES RAID_MAX_STRIPES
+
+enum rg_kind { RG_WRITE_FULL, RG_WRITE_PARTIAL, RG_WRITE_DEGRADED, RG_READ };
+
+enum rg_phase {
+	RG_PHASE_PREREAD,	/* base reads before the parity work */
+	RG_PHASE_GPU,		/* parity work queued or running */
+	RG_PHASE_WRITE,		/* base writes after the parity work */
+	RG_PHASE_READ,		/* plain base reads of a healthy read */
+};
+
+struct rg_info {
+	struct raid_bdev *raid_bdev;
+	struct draid_raid geom;
+	draid_stripe_cache *stripes;	/* per-stripe request queue, shared by the channels */
+	int ngpus;
+	struct raid_gpu_stats stats;
+};
+
+#define RG_COUNT(info, field) __atomic_fetch_add(&(info)->stats.field, 1, __ATOMIC_RELAXED)
+
+static const char *
+rg_level_name(const struct raid_bdev *raid_bdev)
+{
+	/* the framework's name table has no "raid6" entry (bdev_raid.c:880-889) */
+	return raid_bdev->level == RAID5 ? "raid5" : "raid6";
+}
+
+void
+raid_gpu_get_stats(const struct raid_bdev *raid_bdev, struct raid_gpu_stats *stats)
+{
+	const struct rg_info *info = raid_bdev->module_private;
+
+	if (info) {
+		*stats = info->stats;
+	} else {
+		memset(stats, 0, sizeof(*stats));
+	}
+}
+
+struct rg_channel;
+
+struct rg_request {
+	struct rg_channel *ch;
+	struct raid_bdev_io *raid_io;
+	struct spdk_thread *thread;
+	enum rg_kind kind;
+	enum rg_phase phase;
+	struct draid_raid geom;		/* the array's geometry + the degraded mask it runs under */
+	struct draid_stripe_req sreq;
+	struct draid_write_plan plan;
+	struct draid_stripe *stripe;
+	struct draid_stripe_waiter waiter;
+	int gpu;			/* which of the channel's contexts: stripe mod ngpus */
+	uint64_t ticket;
+	int attempts;
+	uint32_t io_failed;		/* disks whose I/O failed in this phase */
+	int remaining;			/* base I/Os of this phase still to complete */
+	int nio, next_io;
+	bool io_write;
+	bool submitting;
+	struct draid_base_io *ios;	/* 3 * n entries */
+	void **chunk_buf;		/* n strip buffers */
+	struct spdk_bdev_io_wait_entry waitq;
+	TAILQ_ENTRY(rg_request) link;
+};
+
+struct rg_channel {
+	struct rg_info *info;
+	draid_ec_ctx *ctx[RG_MAX_GPUS];
+	struct spdk_poller *poller;
+	struct rg_request *requests;
+	uint8_t *pool;			/* RG_MAX_REQUESTS * n strip buffers */
+	TAILQ_HEAD(, rg_request) free_reqs;
+	TAILQ_HEAD(, rg_request) queued;	/* parity work queued on a context, not flushed */
+	TAILQ_HEAD(, rg_request) running;	/* flushed: waiting for the ticket */
+	TAILQ_HEAD(, spdk_bdev_io_wait_entry) waiting;	/* parent I/O waiting for a request */
+};
+
+static void rg_start_request(struct rg_request *req);
+static void rg_submit_ios(struct rg_request *req);
+static void rg_submit_rw_request(struct raid_bdev_io *raid_io);
+
+static inline struct raid_bdev_io_channel *
+rg_raid_ch(struct rg_channel *ch)
+{
+	return (struct raid_bdev_io_channel *)((uint8_t *)ch - sizeof(struct raid_bdev_io_channel));
+}
+
+static uint32_t
+rg_degraded_mask(const struct raid_bdev *raid_bdev)
+{
+	uint32_t mask = 0;
+	uint8_t i;
+
+	for (i = 0; i < raid_bdev->num_base_bdevs; i++) {
+		if (raid_bdev->base_bdev_info[i].degraded) {
+			mask |= 1u << i;
+		}
+	}
+	return mask;
+}
+
+/* The reference's fault-injection hook (bdev_raid.c:1157-1170, commented out
+ * there) as a function: marks a base bdev degraded or healthy again. */
+int
+raid_gpu_set_degraded(struct raid_bdev *raid_bdev, uint8_t slot, bool degraded)
+{
+	uint8_t i;
+	bool any = false;
+
+	if (slot >= raid_bdev->num_base_bdevs) {
+		return -EINVAL;
+	}
+	if (degraded && !raid_bdev->base_bdev_info[slot].degraded &&
+	    __builtin_popcount(rg_degraded_mask(raid_bdev)) >=
+	    raid_bdev->module->base_bdevs_max_degraded) {
+		return -EBUSY;	/* one more than the level tolerates */
+	}
+	raid_bdev->base_bdev_info[slot].degraded = degraded;
+	for (i = 0; i < raid_bdev->num_base_bdevs; i++) {
+		any |= raid_bdev->base_bdev_info[i].degraded;
+	}
+	raid_bdev->degraded = any;
+	return 0;
+}
+
+/* ------------------------------------------------------------ completion */
+
+static void _rg_start_request(void *ctx)
+{
+	rg_start_request(ctx);
+}
+
+static void _rg_resubmit(void *ctx)
+{
+	rg_submit_rw_request(ctx);
+}
+
+/* raid5_complete_stripe_request (raid5.c:485-521): complete the parent I/O, hand
+ * the stripe to its next queued request, give the request back. */
+static void
+rg_complete(struct rg_request *req, enum spdk_bdev_io_status status)
+{
+	struct rg_channel *ch = req->ch;
+	struct rg_info *info = ch->info;
+	struct raid_bdev_io *raid_io = req->raid_io;
+	struct spdk_bdev_io_wait_entry *wqe;
+
+	if (req->stripe) {
+		struct draid_stripe_waiter *next = draid_stripe_complete(info->stripes, req->stripe,
+						   &req->waiter);
+		draid_stripe_put(info->stripes, req->stripe);
+		req->stripe = NULL;
+		if (next) {
+			struct rg_request *nreq = next->arg;
+			/* the next request may live on another channel's thread (raid5.c:501-505) */
+			if (nreq->thread == spdk_get_thread()) {
+				rg_start_request(nreq);
+			} else {
+				spdk_thread_send_msg(nreq->thread, _rg_start_request, nreq);
+			}
+		}
+	}
+	req->raid_io = NULL;
+	TAILQ_INSERT_HEAD(&ch->free_reqs, req, link);
+	raid_bdev_io_complete(raid_io, status);
+	wqe = TAILQ_FIRST(&ch->waiting);
+	if (wqe) {
+		TAILQ_REMOVE(&ch->waiting, wqe, link);
+		wqe->cb_fn(wqe->cb_arg);
+	}
+}
+
+/* ------------------------------------------------------------ base bdev I/O */
+
+static void rg_phase_done(struct rg_request *req);
+
+static void
+rg_io_finished(struct rg_request *req)
+{
+	assert(req->remaining > 0);
+	if (--req->remaining == 0 && !req->submitting) {
+		rg_phase_done(req);
+	}
+}
+
+static void
+rg_chunk_io_done(struct spdk_bdev_io *bdev_io, bool success, void *cb_arg)
+{
+	struct rg_request *req = cb_arg;
+	int disk = -1;
+	uint8_t i;
+
+	/* which disk: the completed I/O's bdev (raid5.c:596-615 gets it from the chunk) */
+	if (bdev_io) {
+		for (i = 0; i < req->geom.num_base_bdevs; i++) {
+			if (req->ch->info->raid_bdev->base_bdev_info[i].bdev == bdev_io->bdev) {
+				disk = i;
+				break;
+			}
+		}
+		spdk_bdev_free_io(bdev_io);
+	}
+	if (!success && disk >= 0) {
+		req->io_failed |= 1u << disk;
+	}
+	rg_io_finished(req);
+}
+
+static void _rg_submit_ios(void *ctx)
+{
+	rg_submit_ios(ctx);
+}
+
+/* raid5_submit_chunk_request (raid5.c:617-689): one spdk_bdev_{read,write}v_blocks
+ * per listed base I/O; -ENOMEM parks the request on the base bdev's io_wait queue
+ * and continues from the same I/O. */
+static void
+rg_submit_ios(struct rg_request *req)
+{
+	struct rg_channel *ch = req->ch;
+	struct raid_bdev *raid_bdev = ch->info->raid_bdev;
+	struct raid_bdev_io_channel *raid_ch = rg_raid_ch(ch);
+
+	req->submitting = true;
+	while (req->next_io < req->nio) {
+		struct draid_base_io *io = &req->ios[req->next_io];
+		struct raid_base_bdev_info *base_info = &raid_bdev->base_bdev_info[io->disk];
+		struct spdk_io_channel *base_ch = raid_ch->base_channel[io->disk];
+		int rc;
+
+		if (req->geom.degraded_mask & (1u << io->disk)) {
+			/* a write to a lost disk: parity carries it (reads never list one) */
+			req->next_io++;
+			req->remaining--;
+			continue;
+		}
+		if (req->io_write) {
+			rc = spdk_bdev_writev_blocks(base_info->desc, base_ch, io->iov, io->iovcnt,
+						     io->offset_blocks, io->num_blocks,
+						     rg_chunk_io_done, req);
+		} else {
+			rc = spdk_bdev_readv_blocks(base_info->desc, base_ch, io->iov, io->iovcnt,
+						    io->offset_blocks, io->num_blocks,
+						    rg_chunk_io_done, req);
+		}
+		if (spdk_unlikely(rc == -ENOMEM)) {
+			req->waitq.bdev = base_info->bdev;
+			req->waitq.cb_fn = _rg_submit_ios;
+			req->waitq.cb_arg = req;
+			spdk_bdev_queue_io_wait(base_info->bdev, base_ch, &req->waitq);
+			req->submitting = false;
+			return;
+		}
+		req->next_io++;
+		if (spdk_unlikely(rc != 0)) {
+			SPDK_ERRLOG("base bdev %d: submit failed: %s\n", io->disk, spdk_strerror(-rc));
+			req->io_failed |= 1u << io->disk;
+			req->remaining--;
+		}
+	}
+	req->submitting = false;
+	if (req->remaining == 0) {
+		rg_phase_done(req);
+	}
+}
+
+static void
+rg_issue(struct rg_request *req, int nio, bool write, enum rg_phase phase)
+{
+	req->phase = phase;
+	req->nio = nio;
+	req->next_io = 0;
+	req->remaining = nio;
+	req->io_write = write;
+	req->io_failed = 0;
+	if (nio == 0) {
+		rg_phase_done(req);
+		return;
+	}
+	rg_submit_ios(req);
+}
+
+/* ------------------------------------------------------------ parity work */
+
+static void
+rg_gpu_queued(struct rg_request *req)
+{
+	req->phase = RG_PHASE_GPU;
+	TAILQ_INSERT_TAIL(&req->ch->queued, req, link);
+}
+
+/* The parity work of a request finished on the GPU. */
+static void
+rg_gpu_done(struct rg_request *req)
+{
+	if (req->kind == RG_READ) {
+		rg_complete(req, SPDK_BDEV_IO_STATUS_SUCCESS);
+		return;
+	}
+	/* ios[] already lists the base writes (filled when the work was queued) */
+	rg_issue(req, req->nio, true, RG_PHASE_WRITE);
+}
+
+static int
+rg_queue_error(struct rg_request *req, int rc, const char *what)
+{
+	SPDK_ERRLOG("stripe %" PRIu64 ": %s failed (%d): %s\n", req->sreq.stripe_index, what, rc,
+		    draid_ec_last_error());
+	return rc;
+}
+
+/* Queues the parity work of a write whose prereads (if any) are in, and lists
+ * its base writes in ios[]. */
+static int
+rg_queue_write(struct rg_request *req)
+{
+	struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(req->raid_io);
+	draid_ec_ctx *ctx = req->ch->ctx[req->gpu];
+	int nw = 0, rc;
+
+	if (req->kind == RG_WRITE_FULL) {
+		void *parity[2] = { req->chunk_buf[req->sreq.p_disk],
+				    req->sreq.q_disk >= 0 ? req->chunk_buf[req->sreq.q_disk] : NULL
+				  };
+
+		rc = draid_raid_stripe_write(&req->geom, ctx, &req->sreq, bdev_io->u.bdev.iovs,
+					     bdev_io->u.bdev.iovcnt, parity, req->ios, &nw);
+		if (rc) {
+			return rg_queue_error(req, rc, "draid_raid_stripe_write");
+		}
+	} else {
+		if (req->kind == RG_WRITE_DEGRADED) {
+			/* every surviving strip is in chunk_buf: rebuild the lost ones there,
+			 * then re-encode the whole strip range over old + new data (the
+			 * reconstruct-write of raid5.c:743-777 with nothing left to read) */
+			rc = draid_raid_stripe_degraded_rebuild(&req->geom, ctx, req->sreq.stripe_index,
+								req->chunk_buf);
+			if (rc) {
+				return rg_queue_error(req, rc, "draid_raid_stripe_degraded_rebuild");
+			}
+			memset(&req->plan, 0, sizeof(req->plan));
+			req->plan.mode = DRAID_WRITE_RCW;
+			req->plan.p_offset = 0;
+			req->plan.p_blocks = req->geom.strip_size;
+		}
+		rc = draid_raid_stripe_write_partial(&req->geom, ctx, &req->sreq, &req->plan,
+						     bdev_io->u.bdev.iovs, bdev_io->u.bdev.iovcnt,
+						     req->chunk_buf, req->ios, &nw);
+		if (rc) {
+			return rg_queue_error(req, rc, "draid_raid_stripe_write_partial");
+		}
+	}
+	req->nio = nw;
+	rg_gpu_queued(req);
+	return 0;
+}
+
+/* ------------------------------------------------------------ phases */
+
+static bool
+rg_absorb_failures(struct rg_request *req)
+{
+	struct raid_bdev *raid_bdev = req->ch->info->raid_bdev;
+	uint32_t failed = req->io_failed;
+	uint8_t i;
+
+	for (i = 0; failed && i < raid_bdev->num_base_bdevs; i++) {
+		if (!(failed & (1u << i))) {
+			continue;
+		}
+		if (raid_gpu_set_degraded(raid_bdev, i, true) != 0) {
+			SPDK_ERRLOG("base bdev %u failed: more failures than %s tolerates\n", i,
+				    rg_level_name(raid_bdev));
+			return false;
+		}
+		SPDK_NOTICELOG("base bdev %u failed: raid bdev %s is degraded\n", i,
+			       raid_bdev->bdev.name);
+	}
+	return true;
+}
+
+static void
+rg_phase_done(struct rg_request *req)
+{
+	if (spdk_unlikely(req->io_failed)) {
+		/* a base bdev failed under this request: mark it degraded and, when the
+		 * level still tolerates that, redo the request against the new state */
+		const bool tolerable = rg_absorb_failures(req);
+
+		if (req->phase == RG_PHASE_WRITE) {
+			/* parity was computed over all the new data: a lost disk's write
+			 * is covered by it */
+			rg_complete(req, tolerable ? SPDK_BDEV_IO_STATUS_SUCCESS :
+				    SPDK_BDEV_IO_STATUS_FAILED);
+			return;
+		}
+		if (!tolerable || ++req->attempts > req->geom.max_degraded + 1) {
+			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+			return;
+		}
+		RG_COUNT(req->ch->info, redone);
+		rg_start_request(req);
+		return;
+	}
+
+	switch (req->phase) {
+	case RG_PHASE_PREREAD:
+		if (req->kind == RG_READ) {
+			/* the surviving ranges are in: rebuild the lost requested range */
+			struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(req->raid_io);
+			int rc = draid_raid_stripe_read_rebuild(&req->geom, req->ch->ctx[req->gpu],
+								&req->sreq, bdev_io->u.bdev.iovs,
+								bdev_io->u.bdev.iovcnt, req->chunk_buf);
+			if (rc) {
+				rg_queue_error(req, rc, "draid_raid_stripe_read_rebuild");
+				rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+				return;
+			}
+			rg_gpu_queued(req);
+		} else if (rg_queue_write(req) != 0) {
+			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+		}
+		break;
+	case RG_PHASE_READ:
+	case RG_PHASE_WRITE:
+		rg_complete(req, SPDK_BDEV_IO_STATUS_SUCCESS);
+		break;
+	default:
+		assert(false);
+		rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+		break;
+	}
+}
+
+/* The request owns its stripe: plan it against the current degraded state
+ * (raid5_submit_stripe_request, raid5.c:948-960). */
+static void
+rg_start_request(struct rg_request *req)
+{
+	struct rg_info *info = req->ch->info;
+	struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(req->raid_io);
+	const int n = req->geom.num_base_bdevs;
+	int nio = 0, rc, ndeg;
+	bool write = bdev_io->type == SPDK_BDEV_IO_TYPE_WRITE;
+
+	req->geom.degraded_mask = rg_degraded_mask(info->raid_bdev);
+	ndeg = __builtin_popcount(req->geom.degraded_mask);
+	if (ndeg > req->geom.max_degraded) {
+		SPDK_ERRLOG("stripe %" PRIu64 ": %d base bdevs degraded, %s tolerates %u\n",
+			    req->sreq.stripe_index, ndeg, rg_level_name(info->raid_bdev),
+			    req->geom.max_degraded);
+		rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+		return;
+	}
+
+	if (!write) {
+		uint32_t lost_requested = 0;
+		int disk;
+
+		req->kind = RG_READ;
+		for (disk = 0; disk < n; disk++) {
+			if ((req->geom.degraded_mask & (1u << disk)) && disk != req->sreq.p_disk &&
+			    disk != req->sreq.q_disk && req->sreq.chunk[disk].req_blocks) {
+				lost_requested |= 1u << disk;
+			}
+		}
+		rc = draid_raid_stripe_read(&req->geom, NULL, &req->sreq, bdev_io->u.bdev.iovs,
+					    bdev_io->u.bdev.iovcnt, req->chunk_buf, req->ios, &nio);
+		if (rc) {
+			rg_queue_error(req, rc, "draid_raid_stripe_read");
+			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+			return;
+		}
+		/* healthy chunks: plain reads into the parent iovecs (raid5.c:933-945);
+		 * a lost requested chunk: the other strips' ranges first, then the rebuild */
+		if (lost_requested) {
+			RG_COUNT(info, degraded_reads);
+		} else {
+			RG_COUNT(info, reads);
+		}
+		rg_issue(req, nio, false, lost_requested ? RG_PHASE_PREREAD : RG_PHASE_READ);
+		return;
+	}
+
+	if (ndeg == 0 && req->sreq.full_stripe) {
+		req->kind = RG_WRITE_FULL;
+		RG_COUNT(info, full_stripe_writes);
+		if (rg_queue_write(req) != 0) {
+			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+		}
+		return;
+	}
+	if (ndeg == 0) {
+		req->kind = RG_WRITE_PARTIAL;
+		rc = draid_raid_plan_write(&req->geom, &req->sreq, &req->plan, req->chunk_buf, req->ios,
+					   &nio);
+		if (rc) {
+			rg_queue_error(req, rc, "draid_raid_plan_write");
+			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+			return;
+		}
+		if (req->plan.mode == DRAID_WRITE_RMW) {
+			RG_COUNT(info, rmw_writes);
+		} else {
+			RG_COUNT(info, rcw_writes);
+		}
+		rg_issue(req, nio, false, RG_PHASE_PREREAD);
+		return;
+	}
+	if (req->sreq.full_stripe) {
+		/* every data strip is new: encode, then skip the writes to lost disks */
+		req->kind = RG_WRITE_FULL;
+		RG_COUNT(info, full_stripe_writes);
+		if (rg_queue_write(req) != 0) {
+			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+		}
+		return;
+	}
+	/* partial write to a degraded array: read every surviving strip, rebuild the
+	 * lost ones, re-encode over old + new data */
+	req->kind = RG_WRITE_DEGRADED;
+	RG_COUNT(info, degraded_writes);
+	rc = draid_raid_stripe_degraded_read(&req->geom, NULL, req->sreq.stripe_index, req->chunk_buf,
+					     req->ios, &nio);
+	if (rc) {
+		rg_queue_error(req, rc, "draid_raid_stripe_degraded_read");
+		rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+		return;
+	}
+	rg_issue(req, nio, false, RG_PHASE_PREREAD);
+}
+
+/* ------------------------------------------------------------ submit */
+
+/* raid5_submit_rw_request (raid5.c:1292-1324): the bdev layer has split the
+ * parent I/O at stripe boundaries (optimal_io_boundary, set in rg_start). */
+static void
+rg_submit_rw_request(struct raid_bdev_io *raid_io)
+{
+	struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(raid_io);
+	struct rg_channel *ch = raid_bdev_io_channel_get_resource(raid_io->raid_ch);
+	struct rg_info *info = raid_io->raid_bdev->module_private;
+	struct rg_request *req;
+	int rc;
+
+	req = TAILQ_FIRST(&ch->free_reqs);
+	if (spdk_unlikely(req == NULL)) {
+		/* all stripe requests in flight: retry when one completes
+		 * (raid5_simple.c:364-370) */
+		struct spdk_bdev_io_wait_entry *wqe = &raid_io->waitq_entry;
+
+		wqe->cb_fn = _rg_resubmit;
+		wqe->cb_arg = raid_io;
+		TAILQ_INSERT_TAIL(&ch->waiting, wqe, link);
+		return;
+	}
+
+	req->geom = info->geom;
+	rc = draid_raid_map_request(&req->geom, bdev_io->u.bdev.offset_blocks,
+				    bdev_io->u.bdev.num_blocks, &req->sreq);
+	if (spdk_unlikely(rc != 0)) {
+		SPDK_ERRLOG("request [%" PRIu64 ", +%" PRIu64 ") does not map onto one stripe\n",
+			    bdev_io->u.bdev.offset_blocks, bdev_io->u.bdev.num_blocks);
+		raid_bdev_io_complete(raid_io, SPDK_BDEV_IO_STATUS_FAILED);
+		return;
+	}
+	req->stripe = draid_stripe_get(info->stripes, req->sreq.stripe_index);
+	if (spdk_unlikely(req->stripe == NULL)) {
+		/* every cached stripe is referenced (raid5.c:1310-1318): retry later */
+		struct spdk_bdev_io_wait_entry *wqe = &raid_io->waitq_entry;
+
+		wqe->cb_fn = _rg_resubmit;
+		wqe->cb_arg = raid_io;
+		TAILQ_INSERT_TAIL(&ch->waiting, wqe, link);
+		return;
+	}
+	TAILQ_REMOVE(&ch->free_reqs, req, link);
+	req->raid_io = raid_io;
+	req->thread = spdk_get_thread();
+	req->gpu = (int)(req->sreq.stripe_index % (uint64_t)info->ngpus);
+	req->attempts = 0;
+	req->io_failed = 0;
+	req->waiter.arg = req;
+	/* requests on one stripe run one at a time, in arrival order
+	 * (raid5.c:1047-1054) */
+	if (draid_stripe_enqueue(info->stripes, req->stripe, &req->waiter) == 1) {
+		rg_start_request(req);
+	}
+}
+
+/* ------------------------------------------------------------ poller */
+
+static void
+rg_fail_queued(struct rg_channel *ch, int gpu)
+{
+	struct rg_request *req, *tmp;
+
+	/* launched pieces may still write the requests' buffers: wait them out */
+	draid_ec_ctx_synchronize(ch->ctx[gpu]);
+	draid_ec_ctx_discard_queued(ch->ctx[gpu]);
+	TAILQ_FOREACH_SAFE(req, &ch->queued, link, tmp) {
+		if (req->gpu != gpu) {
+			continue;
+		}
+		TAILQ_REMOVE(&ch->queued, req, link);
+		rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+	}
+}
+
+/* One launch for everything the reactor iteration queued; requests of a flush
+ * finish when its ticket does. */
+static int
+rg_poll(void *arg)
+{
+	struct rg_channel *ch = arg;
+	struct rg_info *info = ch->info;
+	struct rg_request *req, *tmp;
+	int g, busy = 0;
+
+	for (g = 0; g < info->ngpus; g++) {
+		uint64_t ticket;
+		int rc;
+
+		if (draid_ec_ctx_queued(ch->ctx[g]) == 0) {
+			continue;
+		}
+		busy = 1;
+		rc = draid_ec_ctx_flush_ticket(ch->ctx[g], &ticket);
+		if (spdk_unlikely(rc != 0)) {
+			SPDK_ERRLOG("parity flush failed (%d): %s\n", rc, draid_ec_last_error());
+			rg_fail_queued(ch, g);
+			continue;
+		}
+		RG_COUNT(info, flushes);
+		TAILQ_FOREACH_SAFE(req, &ch->queued, link, tmp) {
+			if (req->gpu != g) {
+				continue;
+			}
+			TAILQ_REMOVE(&ch->queued, req, link);
+			RG_COUNT(info, gpu_requests);
+			req->ticket = ticket;
+			TAILQ_INSERT_TAIL(&ch->running, req, link);
+		}
+	}
+	TAILQ_FOREACH_SAFE(req, &ch->running, link, tmp) {
+		const int rc = draid_ec_ctx_ticket_query(ch->ctx[req->gpu], req->ticket);
+
+		if (rc == 1) {
+			continue;	/* still running (another GPU's requests may be done) */
+		}
+		busy = 1;
+		TAILQ_REMOVE(&ch->running, req, link);
+		if (spdk_unlikely(rc != 0)) {
+			SPDK_ERRLOG("parity work failed (%d): %s\n", rc, draid_ec_last_error());
+			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+			continue;
+		}
+		rg_gpu_done(req);
+	}
+	return busy ? SPDK_POLLER_BUSY : SPDK_POLLER_IDLE;
+}
+
+/* ------------------------------------------------------------ channel, start, stop */
+
+static void
+rg_io_channel_resource_deinit(void *resource)
+{
+	struct rg_channel *ch = resource;
+	int g;
+
+	assert(TAILQ_EMPTY(&ch->queued) && TAILQ_EMPTY(&ch->running) && TAILQ_EMPTY(&ch->waiting));
+	spdk_poller_unregister(&ch->poller);
+	for (g = 0; g < RG_MAX_GPUS; g++) {
+		if (ch->ctx[g]) {
+			draid_ec_ctx_destroy(ch->ctx[g]);
+			ch->ctx[g] = NULL;
+		}
+	}
+	if (ch->requests) {
+		int i;
+
+		for (i = 0; i < RG_MAX_REQUESTS; i++) {
+			free(ch->requests[i].ios);
+			free(ch->requests[i].chunk_buf);
+		}
+		free(ch->requests);
+		ch->requests = NULL;
+	}
+	if (ch->pool) {
+		spdk_dma_free(ch->pool);
+		ch->pool = NULL;
+	}
+}
+
+/* raid5_io_channel_resource_init (raid5.c:1491-1541): the channel's request
+ * pool and strip buffers, plus one context per GPU and the completion poller. */
+static int
+rg_io_channel_resource_init(struct raid_bdev *raid_bdev, void *resource)
+{
+	struct rg_channel *ch = resource;
+	struct rg_info *info = raid_bdev->module_private;
+	const int n = raid_bdev->num_base_bdevs;
+	const size_t strip_bytes = (size_t)raid_bdev->strip_size * raid_bdev->bdev.blocklen;
+	struct raid_base_bdev_info *base_info;
+	size_t alignment = 4096;
+	int i, j, g, dev = 0;
+
+	memset(ch, 0, sizeof(*ch));
+	ch->info = info;
+	TAILQ_INIT(&ch->free_reqs);
+	TAILQ_INIT(&ch->queued);
+	TAILQ_INIT(&ch->running);
+	TAILQ_INIT(&ch->waiting);
+
+	RAID_FOR_EACH_BASE_BDEV(raid_bdev, base_info) {
+		alignment = spdk_max(alignment, spdk_bdev_get_buf_align(base_info->bdev));
+	}
+	ch->pool = spdk_dma_malloc((size_t)RG_MAX_REQUESTS * n * strip_bytes, alignment, NULL);
+	ch->requests = calloc(RG_MAX_REQUESTS, sizeof(*ch->requests));
+	if (!ch->pool || !ch->requests) {
+		goto err;
+	}
+	{
+		/* the strip buffers must be GPU reachable: DMA memory the environment
+		 * registered (or allocated through draid_ec_host_alloc) already is */
+		void *dev_ptr;
+
+		if (draid_ec_device_pointer(ch->pool, (size_t)RG_MAX_REQUESTS * n * strip_bytes,
+					    &dev_ptr) != 0 &&
+		    draid_ec_host_register(ch->pool, (size_t)RG_MAX_REQUESTS * n * strip_bytes) != 0) {
+			SPDK_ERRLOG("strip buffers are not GPU reachable and cannot be registered: %s\n",
+				    draid_ec_last_error());
+			goto err;
+		}
+	}
+	for (i = 0; i < RG_MAX_REQUESTS; i++) {
+		struct rg_request *req = &ch->requests[i];
+
+		req->ch = ch;
+		req->ios = calloc((size_t)3 * n, sizeof(*req->ios));
+		req->chunk_buf = calloc(n, sizeof(*req->chunk_buf));
+		if (!req->ios || !req->chunk_buf) {
+			goto err;
+		}
+		for (j = 0; j < n; j++) {
+			req->chunk_buf[j] = ch->pool + ((size_t)i * n + j) * strip_bytes;
+		}
+		TAILQ_INSERT_TAIL(&ch->free_reqs, req, link);
+	}
+	/* one context per GPU; stripe s runs on context s mod ngpus */
+	draid_ec_device_current(&dev);
+	for (g = 0; g < info->ngpus; g++) {
+		int rc = draid_ec_set_device(g);
+
+		if (rc == 0) {
+			rc = draid_ec_ctx_create(&ch->ctx[g]);
+		}
+		if (rc == 0) {
+			rc = draid_ec_ctx_set_host_pointers(ch->ctx[g], 1);
+		}
+		if (rc != 0) {
+			SPDK_ERRLOG("GPU %d: context creation failed (%d): %s\n", g, rc,
+				    draid_ec_last_error());
+			draid_ec_set_device(dev);
+			goto err;
+		}
+	}
+	draid_ec_set_device(dev);
+	ch->poller = SPDK_POLLER_REGISTER(rg_poll, ch, 0);
+	if (!ch->poller) {
+		goto err;
+	}
+	return 0;
+err:
+	SPDK_ERRLOG("Failed to allocate raid gpu io channel\n");
+	rg_io_channel_resource_deinit(ch);
+	return -ENOMEM;
+}
+
+/* raid5_start (raid5.c:1399-1489) */
+static int
+rg_start(struct raid_bdev *raid_bdev)
+{
+	uint64_t min_blockcnt = UINT64_MAX;
+	struct raid_base_bdev_info *base_info;
+	struct rg_info *info;
+	const char *env = getenv("DRAID_RAID_GPUS");
+	int level = raid_bdev->level == RAID5 ? 5 : 6;
+	int rc, count = 0;
+
+	info = calloc(1, sizeof(*info));
+	if (!info) {
+		SPDK_ERRLOG("Failed to allocate raid gpu info\n");
+		return -ENOMEM;
+	}
+	info->raid_bdev = raid_bdev;
+	RAID_FOR_EACH_BASE_BDEV(raid_bdev, base_info) {
+		min_blockcnt = spdk_min(min_blockcnt, base_info->bdev->blockcnt);
+	}
+	rc = draid_raid_start(&info->geom, level, raid_bdev->num_base_bdevs, raid_bdev->bdev.blocklen,
+			      raid_bdev->strip_size, min_blockcnt);
+	if (rc == 0) {
+		rc = draid_stripe_cache_create(&info->stripes, RG_CACHE_STRIPES);
+	}
+	if (rc != 0) {
+		SPDK_ERRLOG("raid%d over %u base bdevs: invalid geometry\n", level,
+			    raid_bdev->num_base_bdevs);
+		free(info);
+		return rc;
+	}
+	/* stripes spread over the node's GPUs by index (stripe mod G); DRAID_RAID_GPUS
+	 * caps G */
+	if (draid_ec_device_count(&count) != 0 || count < 1) {
+		SPDK_ERRLOG("no GPU: %s\n", draid_ec_last_error());
+		draid_stripe_cache_destroy(info->stripes);
+		free(info);
+		return -ENODEV;
+	}
+	info->ngpus = spdk_min(count, RG_MAX_GPUS);
+	if (env && atoi(env) > 0) {
+		info->ngpus = spdk_min(info->ngpus, atoi(env));
+	}
+
+	raid_bdev->bdev.blockcnt = info->geom.blockcnt;
+	/* one stripe per request: the bdev layer splits at stripe boundaries
+	 * (raid5.c:1427-1428) */
+	raid_bdev->bdev.optimal_io_boundary = info->geom.stripe_blocks;
+	raid_bdev->bdev.split_on_optimal_io_boundary = true;
+	raid_bdev->bdev.write_unit_size = info->geom.stripe_blocks;
+	raid_bdev->module_private = info;
+	return 0;
+}
+
+static void
+rg_stop(struct raid_bdev *raid_bdev)
+{
+	struct rg_info *info = raid_bdev->module_private;
+
+	if (info) {
+		draid_stripe_cache_destroy(info->stripes);
+		free(info);
+		raid_bdev->module_private = NULL;
+	}
+}
+
+static struct raid_bdev_module g_raid6_gpu_module = {
+	.level = RAID6,
+	.base_bdevs_min = 4,
+	.base_bdevs_max_degraded = 2,
+	.io_channel_resource_size = sizeof(struct rg_channel),
+	.start = rg_start,
+	.stop = rg_stop,
+	.submit_rw_request = rg_submit_rw_request,
+	.io_channel_resource_init = rg_io_channel_resource_init,
+	.io_channel_resource_deinit = rg_io_channel_resource_deinit,
+};
+RAID_MODULE_REGISTER(&g_raid6_gpu_module)
+
+#ifdef DRAID_SPDK_WITH_RAID5
+/* The same engine as the RAID5 level (XOR parity only).  Off by default: the
+ * reference's raid5.c registers RAID5 when CONFIG_RAID5=y and the framework
+ * allows one module per level (bdev_raid.c:83-92). */
+static struct raid_bdev_module g_raid5_gpu_module = {
+	.level = RAID5,
+	.base_bdevs_min = 3,
+	.base_bdevs_max_degraded = 1,
+	.io_channel_resource_size = sizeof(struct rg_channel),
+	.start = rg_start,
+	.stop = rg_stop,
+	.submit_rw_request = rg_submit_rw_request,
+	.io_channel_resource_init = rg_io_channel_resource_init,
+	.io_channel_resource_deinit = rg_io_channel_resource_deinit,
+};
+RAID_MODULE_REGISTER(&g_raid5_gpu_module)
+#endif
+
+SPDK_LOG_REGISTER_COMPONENT(bdev_raid_gpu)

@@ -1,0 +1,35 @@
+/*
+ * raid_gpu.h -- what the GPU raid level module (raid_gpu.c) exports besides its
+ * `struct raid_bdev_module` registration.
+ */
+#ifndef DRAID_SPDK_RAID_GPU_H
+#define DRAID_SPDK_RAID_GPU_H
+
+#include "bdev_raid.h"
+
+/* Marks base bdev `slot` of a raid bdev degraded (or healthy again) and keeps
+ * raid_bdev->degraded in step: the setter the reference only has as commented-out
+ * test code (module/bdev/raid/bdev_raid.c:1157-1170).  A hot-remove handler that
+ * keeps the array online calls it instead of raid_bdev_deconfigure
+ * (bdev_raid.c:1333-1365); tests use it to inject disk failures.  Requests
+ * already planned finish under the state they started with.
+ * Returns 0, -EINVAL for a bad slot, -EBUSY when one more degraded disk would
+ * exceed the level's base_bdevs_max_degraded. */
+int raid_gpu_set_degraded(struct raid_bdev *raid_bdev, uint8_t slot, bool degraded);
+
+/* What the module has done on a raid bdev since it started (diagnostics and
+ * tests; summed over the channels). */
+struct raid_gpu_stats {
+	uint64_t full_stripe_writes;	/* parity encoded from new data alone */
+	uint64_t rmw_writes;		/* partial writes by read-modify-write */
+	uint64_t rcw_writes;		/* partial writes by reconstruct-write */
+	uint64_t degraded_writes;	/* partial writes that first rebuilt lost strips */
+	uint64_t reads;			/* reads served by plain base reads */
+	uint64_t degraded_reads;	/* reads that rebuilt a lost requested range */
+	uint64_t redone;		/* requests redone after a base bdev failed under them */
+	uint64_t flushes;		/* launches: one per poller iteration with queued work */
+	uint64_t gpu_requests;		/* requests whose parity work those launches carried */
+};
+void raid_gpu_get_stats(const struct raid_bdev *raid_bdev, struct raid_gpu_stats *stats);
+
+#endif /* DRAID_SPDK_RAID_GPU_H */

@@ -256,6 +256,9 @@ int draid_ec_ctx_set_host_pointers(draid_ec_ctx *ctx, int on);
 int draid_ec_ctx_query(draid_ec_ctx *ctx);
 int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);
 uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last flush */
+/* Drops every queued segment (after a failed flush whose requests the caller
+ * fails instead of retrying).  Work already launched is not affected. */
+int draid_ec_ctx_discard_queued(draid_ec_ctx *ctx);
 
 /* Launch an (op, k, m) group as soon as it holds `segments` queued segments,
  * from inside the queueing call (0 = only at draid_ec_ctx_flush, the default).
@@ -302,6 +305,7 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes *h, const uint8_t *fai
 int draid_ec_abi_version(void);
 const char *draid_ec_last_error(void);
 int draid_ec_set_device(int device);
+int draid_ec_device_current(int *device);
 int draid_ec_device_count(int *count);
 
 int draid_ec_stream_create(void **stream);
@@ -313,6 +317,12 @@ int draid_ec_stream_synchronize(void *stream);
 
 int draid_ec_device_alloc(void **ptr, size_t bytes);
 int draid_ec_device_free(void *ptr);
+/* Host memory the GPU can reach, from the runtime's own pinned allocator (mapped
+ * and portable: every GPU of the process sees it at the same address).  For an
+ * environment's DMA allocator (spdk_dma_malloc) to sit on when the driver
+ * refuses to register memory it did not allocate; 4 KiB aligned. */
+int draid_ec_host_alloc(void **ptr, size_t bytes);
+int draid_ec_host_free(void *ptr);
 /* Pin + map an existing host range (e.g. spdk_dma_malloc hugepages,
  * raid5.c:1340-1342) so kernels and DMA can reach it. */
 int draid_ec_host_register(void *ptr, size_t bytes);
