@@ -155,6 +155,117 @@ def cpu_baseline(k: int, m: int, S: int, failures: str, seconds: float, threads:
                       f"{threads} pthreads"}
 
 
+def run_single_process(args, torch, ec) -> None:
+    """The same step with every device slot driven from one thread (draid_ec_mgpu):
+    slot d holds B stripes in its GPU's HBM (weak scaling) -- the stripes a raid
+    bdev would route to it by index -- and each step fans encode + reconstruct out
+    over the slots' streams; no collective, no peer traffic."""
+    cfg = CONFIGS[args.config]
+    k, m, S = cfg["k"], cfg["m"], cfg["strip_kib"] * 1024
+    n = k + m
+    G = max(1, args.gpus)
+    B = args.stripes or cfg["stripes"]
+    ndev = torch.cuda.device_count()
+    devices = [d % ndev for d in range(G)]
+    ec.lib()
+    mg = ec.MultiGpu(devices)
+    fgen = failure_pairs if cfg["failures"] == "dual" else failure_single
+    bufs, views, tables, batches, fails, fail_nps = [], [], [], [], [], []
+    for d in range(G):
+        dev = torch.device("cuda", devices[d])
+        buf = torch.empty(B * n * S, dtype=torch.uint8, device=dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(0x1234 + d)
+        view = buf.view(B, n, S)
+        view[:, :k] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8, device=dev, generator=g)
+        table = (buf.data_ptr() + torch.arange(B * n, dtype=torch.int64, device=dev) * S).contiguous()
+        fnp = fgen(B, k, 0x1234 ^ (d * B))
+        bufs.append(buf)
+        views.append(view)
+        tables.append(table)
+        batches.append(ec.make_batch(k, m, S, B, table))
+        fail_nps.append(fnp)
+        fails.append(torch.from_numpy(fnp.reshape(-1)).to(dev))
+    for d in range(ndev):
+        torch.cuda.synchronize(d)
+
+    def step():
+        mg.encode(batches)
+        mg.reconstruct(batches, fails)
+
+    for _ in range(args.warmup):
+        step()
+    mg.synchronize()
+    # per-kernel events on slot 0's stream (the stream its kernels are launched on)
+    s0 = torch.cuda.ExternalStream(mg.stream(0), device=torch.device("cuda", devices[0]))
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        # slot 0's kernels are bracketed by events; the other slots run the same step
+        ev[i][0].record(s0)
+        mg.encode(batches)
+        ev[i][1].record(s0)
+        mg.reconstruct(batches, fails)
+        ev[i][2].record(s0)
+    mg.synchronize()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    rec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    verified = None
+    if not args.no_verify:
+        # erase the failed data strips of every stripe on every slot, rebuild, compare
+        goods = []
+        for d in range(G):
+            dev = torch.device("cuda", devices[d])
+            goods.append(views[d][:, :k].clone())
+            si = torch.arange(B, device=dev)
+            for slot in range(2):
+                idx = np.nonzero(fail_nps[d][:, slot] != 0xFF)[0]
+                if len(idx):
+                    ii = torch.from_numpy(idx).to(dev)
+                    lost = torch.from_numpy(fail_nps[d][idx, slot].astype(np.int64)).to(dev)
+                    views[d][si[ii], lost] = 0
+            torch.cuda.synchronize(dev)
+        mg.reconstruct(batches, fails)
+        mg.synchronize()
+        verified = all(bool(torch.equal(views[d][:, :k], goods[d])) for d in range(G))
+        del goods
+    units = 2.0 * k * S * B * G * args.steps
+    value = units / elapsed / GIB
+    enc_bytes = float(n * S * B)
+    rec_bytes = float(reconstruct_bytes_per_stripe(k, m, S, cfg["failures"]) * B)
+    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+    rec_gbs = rec_bytes / (rec_ms * 1e-3) / 1e9
+    pmc, pmc_src = load_pmc(args.config)
+    dominant = "reconstruct" if rec_ms >= enc_ms else "encode"
+    gbs = rec_gbs if dominant == "reconstruct" else enc_gbs
+    out = {
+        "metric": ("GiB/s device-resident RAID6 8+2 encode+reconstruct, 64KiB strips, 1/2/4/8 GPU"
+                   if args.config == "raid6_8p2_64k" else f"GiB/s device-resident {cfg['label']}"),
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": G, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (uniform random bytes, torch Generator seed 0x1234+slot)",
+        "config": {"workload": f"{cfg['label']}, {B} stripes per device slot", "name": args.config,
+                   "k": k, "m": m, "strip_bytes": S, "stripes_per_gpu": B, "stripes_total": B * G,
+                   "failures": cfg["failures"],
+                   "layout": "stripe-major contiguous, device pointer table",
+                   "parallelism": f"ONE process, {G} device slots on GPUs {devices} "
+                                  "(draid_ec_mgpu), stripe-sharded, no collectives"},
+        "breakdown": {"encode_ms_slot0": round(enc_ms, 4), "reconstruct_ms_slot0": round(rec_ms, 4),
+                      "note": "slot 0's events include the host's launches on the other slots"},
+        "roofline": {"bound": "hbm", "kernel": f"k_{dominant}<K={k},M={m}> on slot 0",
+                     "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "traffic": (pmc or {}).get(f"{dominant}_hbm_bytes_per_launch"),
+                     "traffic_source": pmc_src},
+        "verified_roundtrip": verified, "cpu_baseline": None,
+    }
+    mg.close()
+    print(json.dumps(out), flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,6 +286,10 @@ def main() -> None:
     ap.add_argument("--layout", default="stripe_major", choices=["stripe_major", "strip_major"],
                     help="placement of the stripes in HBM (DESIGN.md §3)")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--single-process", action="store_true",
+                    help="drive --gpus device slots from THIS process through draid_ec_mgpu (the "
+                         "shape of an SPDK target: one process, stripes routed to GPUs by index) "
+                         "instead of one rank per GPU; slots beyond the visible GPUs share them")
     ap.add_argument("--dist-backend", default="nccl",
                     help="backend of the timing collectives (nccl = RCCL; gloo only for "
                          "rehearsing several ranks on one GPU)")
@@ -186,6 +301,10 @@ def main() -> None:
     import torch
     import torch.distributed as dist
     import draid_ec as ec
+
+    if args.single_process:
+        run_single_process(args, torch, ec)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

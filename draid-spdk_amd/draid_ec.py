@@ -41,7 +41,14 @@ EXPORTS = (
     "draid_ec_pointer_cache_flush", "draid_ec_ctx_flush_ticket", "draid_ec_ctx_ticket_query",
     "draid_ec_ctx_set_host_pointers", "draid_ec_host_alloc", "draid_ec_host_free",
     "draid_ec_ctx_discard_queued", "draid_ec_device_current",
+    "draid_ec_shard_of", "draid_ec_shard_range", "draid_ec_shard_count",
+    "draid_ec_mgpu_create", "draid_ec_mgpu_destroy", "draid_ec_mgpu_devices",
+    "draid_ec_mgpu_device", "draid_ec_mgpu_stream", "draid_ec_mgpu_encode",
+    "draid_ec_mgpu_reconstruct", "draid_ec_mgpu_encode_strided",
+    "draid_ec_mgpu_reconstruct_strided", "draid_ec_mgpu_query", "draid_ec_mgpu_synchronize",
 )
+
+SHARD_RANGE, SHARD_MOD = 0, 1
 
 
 class HostStripes(C.Structure):
@@ -119,6 +126,24 @@ def lib() -> C.CDLL:
         L.draid_ec_host_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
         L.draid_ec_host_free.argtypes = [vp]
         L.draid_ec_ctx_discard_queued.argtypes = [vp]
+        u64 = C.c_uint64
+        L.draid_ec_shard_of.argtypes = [u64, u64, i32, i32]
+        L.draid_ec_shard_range.argtypes = [u64, i32, i32, C.POINTER(u64), C.POINTER(u64)]
+        L.draid_ec_shard_count.argtypes = [u64, i32, i32, i32]
+        L.draid_ec_shard_count.restype = u64
+        L.draid_ec_mgpu_create.argtypes = [C.POINTER(vp), i32, C.POINTER(i32)]
+        for f in ("draid_ec_mgpu_destroy", "draid_ec_mgpu_devices", "draid_ec_mgpu_query",
+                  "draid_ec_mgpu_synchronize"):
+            getattr(L, f).argtypes = [vp]
+        L.draid_ec_mgpu_device.argtypes = [vp, i32]
+        L.draid_ec_mgpu_stream.argtypes = [vp, i32]
+        L.draid_ec_mgpu_stream.restype = vp
+        L.draid_ec_mgpu_encode.argtypes = [vp, C.POINTER(StripeBatch)]
+        L.draid_ec_mgpu_reconstruct.argtypes = [vp, C.POINTER(StripeBatch), C.POINTER(vp),
+                                                C.POINTER(vp)]
+        L.draid_ec_mgpu_encode_strided.argtypes = [vp, C.POINTER(HostStripes)]
+        L.draid_ec_mgpu_reconstruct_strided.argtypes = [vp, C.POINTER(HostStripes), C.POINTER(vp),
+                                                        C.POINTER(vp)]
         L.draid_ec_host_device_pointer.argtypes = [vp, C.POINTER(vp)]
         L.draid_ec_memcpy_async.argtypes = [vp, vp, C.c_size_t, i32, vp]
         L.draid_ec_set_variant.argtypes = [i32]
@@ -393,6 +418,63 @@ class Ctx:
 
     def set_autoflush(self, segments: int):
         return _check(lib().draid_ec_ctx_set_autoflush(self.h, segments), "ctx_set_autoflush")
+
+
+# ---- several GPUs from one process ----
+
+def shard_of(stripe: int, nstripes: int, ndevices: int, policy: int = SHARD_RANGE) -> int:
+    return lib().draid_ec_shard_of(stripe, nstripes, ndevices, policy)
+
+
+def shard_range(nstripes: int, ndevices: int, device: int):
+    lo, hi = C.c_uint64(), C.c_uint64()
+    rc = lib().draid_ec_shard_range(nstripes, ndevices, device, C.byref(lo), C.byref(hi))
+    if rc:
+        raise DraidError(last_error())
+    return lo.value, hi.value
+
+
+def shard_count(nstripes: int, ndevices: int, device: int, policy: int = SHARD_RANGE) -> int:
+    return lib().draid_ec_shard_count(nstripes, ndevices, device, policy)
+
+
+class MultiGpu:
+    """draid_ec_mgpu: a stream per device slot, every call fans out over the slots."""
+
+    def __init__(self, devices=None):
+        h = C.c_void_p()
+        n = len(devices) if devices is not None else 0
+        arr = (C.c_int * n)(*devices) if devices is not None else None
+        _check(lib().draid_ec_mgpu_create(C.byref(h), n, arr), "mgpu_create")
+        self.h = h.value
+        self.n = lib().draid_ec_mgpu_devices(self.h)
+
+    def close(self):
+        if self.h:
+            lib().draid_ec_mgpu_destroy(self.h)
+            self.h = None
+
+    def device(self, slot):
+        return lib().draid_ec_mgpu_device(self.h, slot)
+
+    def stream(self, slot):
+        return lib().draid_ec_mgpu_stream(self.h, slot)
+
+    def encode(self, batches):
+        arr = (StripeBatch * self.n)(*batches)
+        return _check(lib().draid_ec_mgpu_encode(self.h, arr), "mgpu_encode")
+
+    def reconstruct(self, batches, fails, counters=None):
+        arr = (StripeBatch * self.n)(*batches)
+        f = (C.c_void_p * self.n)(*[_ptr(x) if x is not None else None for x in fails])
+        c = (C.c_void_p * self.n)(*[_ptr(x) for x in counters]) if counters else None
+        return _check(lib().draid_ec_mgpu_reconstruct(self.h, arr, f, c), "mgpu_reconstruct")
+
+    def query(self):
+        return _check(lib().draid_ec_mgpu_query(self.h), "mgpu_query")
+
+    def synchronize(self):
+        return _check(lib().draid_ec_mgpu_synchronize(self.h), "mgpu_synchronize")
 
 
 def set_variant(v: int) -> None:

@@ -299,6 +299,54 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes *h, const uint8_t *fai
                               uint32_t chunk_stripes);
 
 /* ------------------------------------------------------------------------
+ * 2d. Several GPUs from one process
+ *
+ * Stripes are independent (the reference only serialises requests to the same
+ * stripe, raid5.c:1047-1054), so the GPUs of a node share them by index with no
+ * data exchanged between devices.  The benchmark spreads them with one process
+ * per GPU; an SPDK target is one process, so a draid_ec_mgpu drives the same
+ * split from one thread: a stream per device slot, each call enqueues every
+ * slot's shard on its own device and returns without waiting, all devices run
+ * concurrently.  Device slot d's shard (pointer table, strips, fail table,
+ * counter) lives in device d's memory.
+ * ---------------------------------------------------------------------- */
+
+#define DRAID_EC_SHARD_RANGE 0 /* device d owns stripes [n*d/G, n*(d+1)/G)           */
+#define DRAID_EC_SHARD_MOD 1   /* device d owns stripes s with s mod G == d (a bdev's
+                                * stripes, in arrival order)                          */
+
+/* Which device slot owns stripe `stripe` of `nstripes` over `ndevices`; -1 when
+ * out of range.  Pure arithmetic (usable without a GPU). */
+int draid_ec_shard_of(uint64_t stripe, uint64_t nstripes, int ndevices, int policy);
+/* The contiguous range of slot `device`, and how many stripes a slot owns. */
+int draid_ec_shard_range(uint64_t nstripes, int ndevices, int device, uint64_t *lo, uint64_t *hi);
+uint64_t draid_ec_shard_count(uint64_t nstripes, int ndevices, int device, int policy);
+
+typedef struct draid_ec_mgpu draid_ec_mgpu;
+
+/* ndevices <= 0: one slot per visible GPU.  devices (may be NULL: 0, 1, ...)
+ * lists the GPU of each slot; a GPU may appear more than once. */
+int draid_ec_mgpu_create(draid_ec_mgpu **mg, int ndevices, const int *devices);
+int draid_ec_mgpu_destroy(draid_ec_mgpu *mg);
+int draid_ec_mgpu_devices(const draid_ec_mgpu *mg);
+int draid_ec_mgpu_device(const draid_ec_mgpu *mg, int slot);   /* the slot's GPU */
+void *draid_ec_mgpu_stream(draid_ec_mgpu *mg, int slot);
+
+/* One batch / descriptor per slot (nstripes == 0: nothing for that device);
+ * fail[d] and unrecoverable[d] as in draid_ec_reconstruct_status, in slot d's
+ * memory (unrecoverable may be NULL altogether). */
+int draid_ec_mgpu_encode(draid_ec_mgpu *mg, const draid_ec_stripe_batch *batches);
+int draid_ec_mgpu_reconstruct(draid_ec_mgpu *mg, const draid_ec_stripe_batch *batches,
+                              const uint8_t *const *fail, uint32_t *const *unrecoverable);
+int draid_ec_mgpu_encode_strided(draid_ec_mgpu *mg, const draid_ec_strided_stripes *shards);
+int draid_ec_mgpu_reconstruct_strided(draid_ec_mgpu *mg, const draid_ec_strided_stripes *shards,
+                                      const uint8_t *const *fail,
+                                      uint32_t *const *unrecoverable);
+/* 0 = every device idle, 1 = some still running, < 0 = error. */
+int draid_ec_mgpu_query(draid_ec_mgpu *mg);
+int draid_ec_mgpu_synchronize(draid_ec_mgpu *mg);
+
+/* ------------------------------------------------------------------------
  * 3. Runtime helpers (device, streams, memory)
  * ---------------------------------------------------------------------- */
 

@@ -69,6 +69,70 @@ def test_shard_range_partitions():
             assert seen == list(range(total))
 
 
+def test_c_abi_split_is_a_partition_and_agrees_with_the_bench():
+    """draid_ec_shard_of / _range / _count (the split a single-process target uses,
+    draid_ec_mgpu) own every stripe exactly once under both policies; the range
+    policy is the bench's per-rank split."""
+    import draid_ec as ec
+    for total in (1, 7, 37, 4096, 16384, (1 << 40) + 3):
+        for g in (1, 2, 3, 8):
+            ranges = [ec.shard_range(total, g, d) for d in range(g)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+            if total <= 16384:
+                assert ranges == [bench.shard_range(total, d, g) for d in range(g)]
+            for pol in (ec.SHARD_RANGE, ec.SHARD_MOD):
+                assert sum(ec.shard_count(total, g, d, pol) for d in range(g)) == total
+            probe = range(total) if total <= 4096 else [0, 1, total // 3, total // 2, total - 2,
+                                                        total - 1]
+            for s in probe:
+                d = ec.shard_of(s, total, g, ec.SHARD_RANGE)
+                assert ranges[d][0] <= s < ranges[d][1]
+                assert ec.shard_of(s, total, g, ec.SHARD_MOD) == s % g
+            assert ec.shard_of(total, total, g, ec.SHARD_RANGE) == -1
+
+
+def _mod_worker(rank, world, port, q):
+    """Rank r plays device slot r of a single-process target: it takes the stripes the
+    C ABI routes to it (s mod G), encodes them, and the union is the whole volume."""
+    import draid_ec as ec
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = [s for s in range(B_TOTAL) if ec.shard_of(s, B_TOTAL, world, ec.SHARD_MOD) == rank]
+    assert len(mine) == ec.shard_count(B_TOTAL, world, rank, ec.SHARD_MOD)
+    allb = _stripes(0, B_TOTAL)
+    buf = np.ascontiguousarray(allb[mine])
+    assert oracle.encode_strided(buf.reshape(-1), K, M, L, len(mine), L, (K + M) * L) == 0
+    parts = [None] * world
+    dist.all_gather_object(parts, (mine, _digest(buf)))
+    if rank == 0:
+        q.put(parts)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_with_the_mod_split_cover_the_volume():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_mod_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = _stripes(0, B_TOTAL)
+    assert oracle.encode_strided(single.reshape(-1), K, M, L, B_TOTAL, L, (K + M) * L) == 0
+    want = _digest(single)
+    got = {}
+    for mine, digests in parts:
+        for s, d in zip(mine, digests):
+            assert s not in got
+            got[s] = d
+    assert [got[s] for s in range(B_TOTAL)] == want
+
+
 def test_two_rank_shards_match_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
