@@ -136,6 +136,15 @@ def cpu_baseline(k: int, m: int, S: int, failures: str, seconds: float, threads:
     if value is None:
         return {"value": None, "error": "oracle bench failed"}
     one, _, _ = run(buf, fail, B, 1, max(1.0, seconds / 4))
+    # every core the process may run on (the GPU box's share is 16 of them; the
+    # host has many more, shared with other tenants), beside the 16 and the 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or threads
+    allc = None
+    if affinity > threads:
+        allc, _, _ = run(buf, fail, B, min(affinity, 512), max(1.0, seconds / 4))
     # the same work streaming from DRAM, as the full-size workload would run on the host
     B2 = max(64, (1 << 30) // ((k + m) * S))
     del buf
@@ -147,6 +156,8 @@ def cpu_baseline(k: int, m: int, S: int, failures: str, seconds: float, threads:
             "64-bit SWAR restatement of isa-l pq_gen_base + nibble-table gf_vect_mul, -O3 -mavx2")
     return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "single_core_value": round(one, 3) if one else None,
+            "all_cores_value": round(allc, 3) if allc else None,
+            "all_cores": min(affinity, 512) if allc else None,
             "dram_resident_value": round(dram, 3) if dram else None,
             "dram_resident_sample": f"{B2} stripes ({(k + m) * S * B2 >> 20} MiB), {passes2} "
                                     f"passes in {el2:.1f}s, {threads} pthreads",
@@ -286,6 +297,11 @@ def main() -> None:
     ap.add_argument("--layout", default="stripe_major", choices=["stripe_major", "strip_major"],
                     help="placement of the stripes in HBM (DESIGN.md §3)")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--stripe-pad", type=int, default=0,
+                    help="lab runs only: bytes added to the stripe pitch of the stripe-major layout "
+                         "(stripe s at s * ((k+m) * S + pad)); 0 = the BASELINE layout")
+    ap.add_argument("--strip-pad", type=int, default=0,
+                    help="lab runs only: bytes added between the strips of a stripe")
     ap.add_argument("--single-process", action="store_true",
                     help="drive --gpus device slots from THIS process through draid_ec_mgpu (the "
                          "shape of an SPDK target: one process, stripes routed to GPUs by index) "
@@ -340,13 +356,18 @@ def main() -> None:
     # Stripes in HBM.  stripe_major: stripe s = [D0 .. D{k-1} P Q], strips contiguous
     # (one stripe-cache slot per stripe); strip_major: one region per strip index j
     # holding strip j of every stripe.  The kernels only see the pointer table.
-    buf = torch.empty(B * n * S, dtype=torch.uint8, device=dev)
+    strip_pitch = S + args.strip_pad
+    stripe_pitch = n * strip_pitch + args.stripe_pad
+    buf = torch.empty(B * stripe_pitch, dtype=torch.uint8, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(0x1234 + rank)
     base = buf.data_ptr()
     if args.layout == "stripe_major":
-        view = buf.view(B, n, S)
-        table = (base + torch.arange(B * n, dtype=torch.int64, device=dev) * S).contiguous()
+        # [stripe, strip, byte] over the (possibly padded) pitches
+        view = buf.as_strided((B, n, S), (stripe_pitch, strip_pitch, 1))
+        si = torch.arange(B, dtype=torch.int64, device=dev).repeat_interleave(n)
+        sj = torch.arange(n, dtype=torch.int64, device=dev).repeat(B)
+        table = (base + si * stripe_pitch + sj * strip_pitch).contiguous()
     else:
         view = buf.view(n, B, S).permute(1, 0, 2)  # [stripe, strip, byte] over the regions
         si = torch.arange(B, dtype=torch.int64, device=dev).repeat_interleave(n)
@@ -455,7 +476,9 @@ def main() -> None:
             "stripes_total": total,
             "failures": cfg["failures"],
             "layout": ("stripe-major contiguous" if args.layout == "stripe_major" else
-                       "strip-major (one region per strip index)") + ", device pointer table",
+                       "strip-major (one region per strip index)") + ", device pointer table" +
+                      (f", stripe pitch +{args.stripe_pad} B, strip pitch +{args.strip_pad} B"
+                       if args.stripe_pad or args.strip_pad else ""),
             "parallelism": f"stripe-sharded x{world}, no collectives",
         },
         **({"lab_variant": args.variant} if args.variant else {}),
