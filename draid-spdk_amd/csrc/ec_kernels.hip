@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ec_gf.hpp"
 #include "ec_launch.hpp"
 
@@ -42,9 +44,14 @@ int get_variant() { return g_variant; }
 struct TablePtrs {
     const uint8_t* const* tab;
     uint32_t stride;
+    // Read through the constant address space: the table is input only, and a
+    // constant-space read at a wave-uniform index is always a scalar load (an
+    // ordinary global read becomes a per-lane load as soon as any store, atomic,
+    // LDS write or barrier precedes it, and its pointer then lives in VGPRs).
     __device__ __forceinline__ const uint8_t* get(uint32_t s, int j) const
     {
-        return tab[(size_t)s * stride + j];
+        typedef const uint8_t* const __attribute__((address_space(4)))* ctab;
+        return ((ctab)(uintptr_t)tab)[(size_t)s * stride + j];
     }
 };
 
@@ -146,6 +153,34 @@ struct Mem<uint32_t> {
     static __device__ __forceinline__ bool any(uint32_t v) { return (v & 0xffu) != 0; }
 };
 
+// ND (1 or 2) consecutive dwords at a byte offset, with the store policy of POL.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <int POL, int ND>
+__device__ __forceinline__ void st_words(const uint8_t* p, uint32_t byte_off,
+                                         const uint32_t (&v)[ND])
+{
+    static_assert(ND == 1 || ND == 2, "a dword or a pair");
+    constexpr int aux = (POL >> 16) & 0xff;
+    if constexpr (aux != 0) {
+        if constexpr (ND == 1)
+            __builtin_amdgcn_raw_buffer_store_b32(v[0], Mem<u32x4>::rsrc(p),
+                                                  static_cast<int>(byte_off), 0, aux - 1);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, Mem<u32x4>::rsrc(p),
+                                                  static_cast<int>(byte_off), 0, aux - 1);
+    } else {
+        typedef uint32_t __attribute__((address_space(1)))* gw;
+        gw q = (gw)(const_cast<uint8_t*>(p) + byte_off);
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+            if constexpr ((POL & 2) != 0)
+                __builtin_nontemporal_store(v[n], q + n);
+            else
+                q[n] = v[n];
+        }
+    }
+}
+
 // Calls f(j) for j = k-1 down to 0; fully unrolled when k is a template constant.
 template <int KT, class F>
 __device__ __forceinline__ void for_sources_desc(int k, F&& f)
@@ -239,10 +274,16 @@ __device__ __forceinline__ bool stripe_aligned(const Ptrs& pp, uint32_t s, int k
 //         is worth more to these streaming kernels than the extra latency
 //         hiding (8+2 x 64 KiB dual reconstruct: 0.411 ms at 5 waves, 0.420 at
 //         the 7 its 70 VGPRs would allow, 0.417 at 4).
-template <int NTHR_, int U_, int POL_, int MAP_, int PLAN_ = 0, int WAVES_ = 0>
+//   SPLIT waves that share one item: the workgroup has SPLIT * 64 lanes, the item
+//         is still 64 lanes wide (1 KiB of every strip at U = 1), and wave w loads
+//         only strips [w*KW, (w+1)*KW), KW = ceil(k / SPLIT); the partial sums meet
+//         in LDS (k_encode_split / k_reconstruct_split).  NTHR_ counts the lanes of
+//         the whole workgroup.
+template <int NTHR_, int U_, int POL_, int MAP_, int PLAN_ = 0, int WAVES_ = 0, int SPLIT_ = 1>
 struct Cfg {
     static constexpr int NTHR = NTHR_, U = U_, POL = POL_, MAP = MAP_, PLAN = PLAN_,
-                         WAVES = WAVES_;
+                         WAVES = WAVES_, SPLIT = SPLIT_, ITEM = NTHR_ / SPLIT_;
+    static_assert(SPLIT_ == 1 || (NTHR_ == 64 * SPLIT_ && U_ == 1), "a split item is one wave wide");
 };
 #define DRAID_WAVES_PER_EU(C) \
     __attribute__((amdgpu_waves_per_eu((C::WAVES) ? (C::WAVES) : 1, (C::WAVES) ? (C::WAVES) : 8)))
@@ -340,52 +381,79 @@ struct RecPlan {
     bool needq;        // the Q syndrome over the survivors is needed
     bool skip;         // unrecoverable / nothing to do
     bool bad;          // more failures than M parities, or an index outside the stripe
+    uint32_t lost;     // bit j set: strip j is lost (decode_failures_mask only)
     MulTable t1, t2;   // constant multipliers (see plan_constants)
 };
 
+// The stripe's two failure bytes, fail[2s] | fail[2s+1] << 8, through aligned word
+// reads at a wave-uniform address -- scalar loads.  A byte load would be a vector
+// memory instruction, and an item whose first instruction waits a full memory
+// round trip before the plan is known, and only then issues its strip loads,
+// takes half as long again.
+__device__ __forceinline__ uint32_t load_fail_pair(const uint8_t* fail, uint32_t s)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(fail) + 2 * static_cast<uintptr_t>(s);
+    // constant address space: the table is input only, never written by the kernel
+    typedef const uint32_t __attribute__((address_space(4)))* ccw;
+    const ccw w = (ccw)(a & ~static_cast<uintptr_t>(3));
+    const uint32_t at = static_cast<uint32_t>(a) & 3u;
+    uint32_t v = w[0] >> (at * 8u);
+    if (at == 3u)  // the pair straddles two words (a table at an odd address)
+        v |= w[1] << 8;
+    return v & 0xffffu;
+}
+
 // Decodes the (wave-uniform) failure pair: which strips are lost, which
-// syndromes are needed.  No table lookups -- runs before any load is issued.
+// syndromes are needed.  No table lookups -- runs before any load is issued, on
+// the scalar unit, so it is written without branches: every wave of every item
+// runs it ahead of its first strip load.
 template <int M>
 __device__ __forceinline__ RecPlan decode_failures(int k, uint32_t f0, uint32_t f1)
 {
     RecPlan pl;
-    pl.x = -1;
-    pl.y = -1;
-    pl.nd = 0;
-    pl.lostP = false;
-    pl.lostQ = false;
-    bool oob = false;
-    const uint32_t f[2] = {static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(f0)),
-                           static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(f1))};
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int j = static_cast<int>(f[t]);
-        if (f[t] == 0xffu)
-            continue;
-        if (j >= k + M) {
-            oob = true;
-            continue;
-        }
-        if (j < k) {
-            if (pl.nd == 1 && pl.x == j)
-                continue;
-            if (pl.nd == 0)
-                pl.x = j;
-            else
-                pl.y = j;
-            ++pl.nd;
-        } else if (j == k) {
-            pl.lostP = true;
-        } else {
-            pl.lostQ = true;
-        }
-    }
-    if (pl.nd == 2 && pl.x > pl.y) {
-        const int t = pl.x;
-        pl.x = pl.y;
-        pl.y = t;
-    }
+    constexpr int kNone = 0x7fffffff;  // 0xff: no failure in this slot
+    const int ra = static_cast<int>(__builtin_amdgcn_readfirstlane(f0));
+    const int rb = static_cast<int>(__builtin_amdgcn_readfirstlane(f1));
+    const int a = ra == 0xff ? kNone : ra, b = rb == 0xff ? kNone : rb;
+    const bool da = a < k, db = b < k && b != a;  // lost data strips
+    pl.nd = (da ? 1 : 0) + (db ? 1 : 0);
+    const int lo = da ? a : (db ? b : -1);
+    const int hi = (da && db) ? b : -1;
+    pl.x = (hi >= 0 && hi < lo) ? hi : lo;
+    pl.y = (hi >= 0 && hi < lo) ? lo : hi;
+    pl.lostP = a == k || b == k;
+    pl.lostQ = a == k + 1 || b == k + 1;
+    const bool oob = (a != kNone && a >= k + M) || (b != kNone && b >= k + M);
+    if (M == 1)
+        pl.lostQ = false;  // index k + 1 is outside a RAID5 stripe (counted by oob)
     const int nf = pl.nd + (pl.lostP ? 1 : 0) + (pl.lostQ ? 1 : 0);
+    pl.skip = (nf == 0) || (nf > M);
+    pl.bad = oob || nf > M;
+    pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
+    return pl;
+}
+
+// The same decode for a stripe of at most 32 strips known at compile time, over a
+// bit mask of the lost strips: a third of the scalar instructions, and "is strip
+// j lost" becomes a one-instruction bit test per load.  Every wave of a split
+// item runs this ahead of its strip loads, so its length is item latency.
+template <int K, int M>
+__device__ __forceinline__ RecPlan decode_failures_mask(uint32_t f0, uint32_t f1)
+{
+    static_assert(K + M <= 32, "one mask word");
+    constexpr uint32_t N = K + M, DATA = (K >= 32) ? 0xffffffffu : ((1u << K) - 1u);
+    RecPlan pl;
+    const uint32_t a = __builtin_amdgcn_readfirstlane(f0), b = __builtin_amdgcn_readfirstlane(f1);
+    const uint32_t L = (a < N ? 1u << a : 0u) | (b < N ? 1u << b : 0u);
+    const bool oob = (a >= N && a != 0xffu) || (b >= N && b != 0xffu);
+    const uint32_t D = L & DATA;
+    pl.lost = L;
+    pl.nd = __builtin_popcount(D);
+    pl.x = __builtin_ffs(static_cast<int>(D)) - 1;                  // lowest lost data strip, or -1
+    pl.y = pl.nd == 2 ? 31 - __builtin_clz(D) : -1;
+    pl.lostP = (L >> K) & 1u;
+    pl.lostQ = M == 2 && ((L >> (K + 1)) & 1u);
+    const int nf = __builtin_popcount(L);
     pl.skip = (nf == 0) || (nf > M);
     pl.bad = oob || nf > M;
     pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
@@ -496,6 +564,85 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
     }
 }
 
+// Tables for the plan's constants, read with wave-uniform indices through scalar
+// loads (their own counter: they complete while the strip loads are in flight,
+// with no LDS staging and no barrier).
+//   lden[d]  log of 1 / (2^d ^ 1), 0 < d < 255 -- the one inverse of the D+D
+//            constants (gf_vect_mul.c:296-326), as a word image of a byte table
+//   mul[i]   the MulTable of the constant 2^i (5 words used of 8), i < 255
+// Every constant of a plan is a power of two (2^x, 2^-x, A = 2^(d + lden[d]),
+// B = 2^(255 - x + lden[d])), so its table is one 32-byte read by exponent
+// instead of ~55 scalar operations building it.
+struct PlanTables {
+    uint32_t lden[64];
+    uint32_t mul[255][8];
+};
+
+constexpr PlanTables make_plan_tables()
+{
+    const GfTables g = make_gf_tables();
+    PlanTables t{};
+    for (int d = 1; d < 255; ++d) {
+        const uint32_t l = (255u - g.log[g.exp[d] ^ 1u]) % 255u;
+        t.lden[d >> 2] |= l << ((d & 3) * 8);
+    }
+    for (int i = 0; i < 255; ++i) {
+        uint32_t p[8] = {};
+        for (int b = 0; b < 8; ++b)
+            p[b] = g.exp[i + b];  // 2^i * 2^b
+        // same layout as make_mul_table / tri_words
+        t.mul[i][0] = (p[0] << 8) | (p[1] << 16) | ((p[0] ^ p[1]) << 24);
+        t.mul[i][1] = t.mul[i][0] ^ (p[2] * 0x01010101u);
+        t.mul[i][2] = (p[3] << 8) | (p[4] << 16) | ((p[3] ^ p[4]) << 24);
+        t.mul[i][3] = t.mul[i][2] ^ (p[5] * 0x01010101u);
+        t.mul[i][4] = (p[6] << 8) | (p[7] << 16) | ((p[6] ^ p[7]) << 24);
+    }
+    return t;
+}
+
+__constant__ PlanTables c_plan = make_plan_tables();
+
+__device__ __forceinline__ uint32_t word_byte(const uint32_t* t, uint32_t idx)
+{
+    return (t[idx >> 2] >> ((idx & 3u) << 3)) & 0xffu;
+}
+
+// MulTable of 2^e, e < 510.
+__device__ __forceinline__ MulTable mul_table_exp2(uint32_t e)
+{
+    e = e >= 255u ? e - 255u : e;
+    const uint32_t* w = c_plan.mul[e];
+    MulTable t;
+    t.t0[0] = w[0];
+    t.t0[1] = w[1];
+    t.t1[0] = w[2];
+    t.t1[1] = w[3];
+    t.t2 = w[4];
+    return t;
+}
+
+// The plan's two multiplication tables from scalar reads of c_plan; the same
+// constants as plan_constants.
+struct PlanMul {
+    MulTable t1, t2;
+};
+__device__ __forceinline__ PlanMul plan_constants_scalar(int nd, int x, int y, bool lostP,
+                                                         bool lostQ)
+{
+    PlanMul m{};
+    if (nd == 1 && !lostP && lostQ) {
+        m.t1 = mul_table_exp2(x);                          // Q = Qs ^ 2^x D_x
+    } else if (nd == 1 && lostP) {
+        m.t1 = mul_table_exp2(255u - x);                   // D_x = 2^-x (Q ^ Qs)
+    } else if (nd == 2) {
+        const uint32_t d = static_cast<uint32_t>(y - x);
+        const uint32_t l = word_byte(c_plan.lden, d);
+        m.t1 = mul_table_exp2(d + l);                      // A = 2^(y-x) / (2^(y-x) ^ 1)
+        m.t2 = mul_table_exp2(255u - x + l);               // B = 2^-x / (2^(y-x) ^ 1)
+    }
+    return m;
+}
+
 // LDS image of the exp/log tables (768 B).
 struct LdsGf {
     uint32_t w[(512 + 256) / 4];
@@ -527,7 +674,7 @@ struct TabStage {
             w[i] = t < kWords ? reinterpret_cast<const uint32_t*>(&c_gf)[t] : 0u;
         }
     }
-    __device__ __forceinline__ void store(LdsGf& lds) const
+    __device__ __forceinline__ void put(LdsGf& lds) const
     {
 #pragma unroll
         for (int i = 0; i < kPerLane; ++i) {
@@ -535,6 +682,10 @@ struct TabStage {
             if (t < kWords)
                 lds.w[t] = w[i];
         }
+    }
+    __device__ __forceinline__ void store(LdsGf& lds) const
+    {
+        put(lds);
         __syncthreads();
     }
 };
@@ -599,16 +750,22 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
         item_coords<C>(b, cps, nstripes, s, c);
         uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
         if (fail) {
-            f0 = fail[2 * (size_t)s];
-            f1 = fail[2 * (size_t)s + 1];
+            const uint32_t f = load_fail_pair(fail, s);
+            f0 = f & 0xffu;
+            f1 = f >> 8;
         }
         RecPlan pl = decode_failures<M>(k, f0, f1);
         // A stripe that cannot be rebuilt is left untouched and counted once (by
         // the workgroup of its first chunk) when the caller asked for the count.
-        if (bad && pl.bad && c == 0 && threadIdx.x == 0)
-            atomicAdd(bad, 1u);
-        if (pl.skip)
+        // Skipped stripes are the only ones counted before any load: a store or
+        // atomic ahead of the pointer-table reads would keep them from being
+        // scalar loads.
+        const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
+        if (pl.skip) {
+            if (count_bad)
+                atomicAdd(bad, 1u);
             continue;  // uniform across the workgroup
+        }
         if constexpr (C::PLAN == 2 || C::PLAN == 3) {
             // DIAGNOSTIC ONLY (tools/sweep.py): constants left zero, no LDS, no
             // barrier -- wrong results, measures what the plan step costs.
@@ -631,7 +788,371 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
                 plan_constants(p, l_exp, l_log);
             });
         }
+        if (count_bad)
+            atomicAdd(bad, 1u);
     }
+}
+
+// ------------------------------------------------------------ split items
+//
+// The same item (1 KiB of every strip of one stripe) shared by SPLIT waves of one
+// workgroup.  A wave that loads all k strips of an item keeps k KiB in flight and
+// holds its slot until the last of them has arrived; the CU then either has few
+// waves (idle slots while workgroups turn over) or far more bytes in flight than
+// the memory system needs, and DRAM efficiency falls as k grows (16+2: 6.0 TB/s).
+// With the strips of the item dealt over 3-4 waves every wave has 2-4 loads, a CU
+// holds 6 items instead of 16-24, and the same shapes stream 5-7% faster
+// (tools/probe/wide_probe.hip: 8+2 x 64 KiB 6.96 vs 6.64 TB/s, 16+2 x 256 KiB
+// 6.42 vs 6.00).  Wave w accumulates P and the Horner form of Q over its strips
+// [w*KW, (w+1)*KW), scales its Q part by 2^(w*KW), and the parts are XORed
+// through LDS after one barrier.
+
+// Split kernels take a 2-D/3-D grid -- x the chunk, y (and z beyond 65535) the
+// stripe -- so an item's coordinates cost no division.
+constexpr uint32_t kGridY = 65535;
+
+template <int SPLIT>
+struct SplitLds {
+    u32x4 p[SPLIT][64];
+    u32x4 q[SPLIT][64];
+};
+
+// 2^e in GF(2^8); e is a compile-time constant wherever this is used, so the
+// multiplication table built from it folds into immediates.
+__host__ __device__ constexpr uint32_t gf_exp2_const(int e)
+{
+    uint32_t c = 1;
+    for (int i = 0; i < e; ++i)
+        c = ((c << 1) ^ ((c & 0x80u) ? 0x1du : 0u)) & 0xffu;
+    return c;
+}
+
+// Partial sums of one wave (and, in the reconstruct, the plan's tables).
+struct PartPQ {
+    u32x4 p, q;
+};
+struct PartRec {
+    u32x4 p, q;
+    PlanMul mul;
+};
+
+// Returns part(std::integral_constant<int, W>) for the wave's own index W = w
+// (wave-uniform, scalar branches).  Each wave gets code specialised for its
+// strips: strip indices are constants, so a pointer table row is fetched with
+// scalar loads of fixed offsets (a run-time strip index turns them into per-lane
+// loads plus a readfirstlane loop around every strip access).  The parts come
+// back by value -- sums captured by reference end up in scratch memory.
+template <int W, int SPLIT, class F>
+__device__ __forceinline__ auto wave_case(uint32_t w, const F& part)
+{
+    if constexpr (W + 1 == SPLIT) {
+        return part(std::integral_constant<int, W>{});
+    } else {
+        if (w == W)
+            return part(std::integral_constant<int, W>{});
+        return wave_case<W + 1, SPLIT>(w, part);
+    }
+}
+
+template <int SPLIT>
+__device__ __forceinline__ u32x4 split_sum(const u32x4 (&part)[SPLIT][64], uint32_t lane)
+{
+    u32x4 a = part[0][lane];
+#pragma unroll
+    for (int t = 1; t < SPLIT; ++t)
+        a ^= part[t][lane];
+    return a;
+}
+
+// Vector i of every strip: wave 0 ends up storing (or checking) P, the last wave Q.
+template <int KT, int M, int SPLIT, int POL, bool CHECK, bool BOUNDED, class Ptrs>
+__device__ __forceinline__ bool encode_split_vec(const Ptrs& pp, uint32_t s, uint32_t w,
+                                                 uint32_t lane, uint32_t i, uint32_t nvec,
+                                                 SplitLds<SPLIT>& lds)
+{
+    using MW = Mem<u32x4>;
+    constexpr int KW = (KT + SPLIT - 1) / SPLIT;
+    const bool ok = !BOUNDED || i < nvec;
+    // Every pointer is fetched before the barrier: a table read after it can no
+    // longer be a scalar load (LDS writes and the barrier count as clobbers).
+    const uint8_t* dp = pp.get(s, KT);
+    const uint8_t* dq = (M == 2) ? pp.get(s, KT + 1) : dp;
+    const PartPQ part = wave_case<0, SPLIT>(w, [=, &pp](auto wc) __attribute__((always_inline)) {
+        constexpr int J0 = decltype(wc)::value * KW;
+        u32x4 p = 0, q = 0;
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j) {
+            u32x4 d = 0;
+            if (J0 + j < KT && ok)
+                d = MW::template ld<POL>(pp.get(s, J0 + j), i);
+            p ^= d;
+            if constexpr (M == 2)
+                q = gf_mul2(q) ^ d;
+        }
+        if constexpr (M == 2 && J0 != 0)
+            q = gf_mulc(make_mul_table(gf_exp2_const(J0)), q);
+        return PartPQ{p, q};
+    });
+    lds.p[w][lane] = part.p;
+    if constexpr (M == 2)
+        lds.q[w][lane] = part.q;
+    __syncthreads();
+    bool bad = false;
+    if (w == 0) {
+        const u32x4 a = split_sum<SPLIT>(lds.p, lane);
+        if (ok) {
+            if constexpr (CHECK)
+                bad = MW::any(MW::template ld<0>(dp, i) ^ a);
+            else
+                MW::template st<POL>(dp, i, a);
+        }
+    }
+    if constexpr (M == 2) {
+        if (w == SPLIT - 1) {
+            const u32x4 a = split_sum<SPLIT>(lds.q, lane);
+            if (ok) {
+                if constexpr (CHECK)
+                    bad = MW::any(MW::template ld<0>(dq, i) ^ a);
+                else
+                    MW::template st<POL>(dq, i, a);
+            }
+        }
+    }
+    return bad;
+}
+
+// The 16-byte vectors go through the split path; a byte tail (len % 16) and
+// strips that are not 16-byte aligned take the one-wave byte path on wave 0.
+template <int KT, int M, bool CHECK, class C, class Ptrs>
+__device__ __forceinline__ bool encode_item_split(const Ptrs& pp, uint32_t s, uint32_t c,
+                                                  uint32_t len, uint32_t cps,
+                                                  SplitLds<C::SPLIT>& lds)
+{
+    constexpr int SPLIT = C::SPLIT, POL = C::POL;
+    constexpr uint32_t L = 64;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t nvec = len >> 4;
+    bool bad = false;
+    if (stripe_aligned<KT, M>(pp, s, KT)) {
+        const uint32_t i = c * L + lane;
+        if ((c + 1) * L <= nvec)
+            bad = encode_split_vec<KT, M, SPLIT, POL, CHECK, false>(pp, s, w, lane, i, nvec, lds);
+        else
+            bad = encode_split_vec<KT, M, SPLIT, POL, CHECK, true>(pp, s, w, lane, i, nvec, lds);
+        const uint32_t tail = len & 15u;
+        if (w == 0 && tail && c == cps - 1 && lane < tail)
+            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(pp, s, KT, nvec * 16 + lane, L,
+                                                                    len);
+    } else if (w == 0) {
+        const uint32_t b1 = min(len, (c + 1) * L * 16);
+        for (uint32_t b = c * L * 16 + lane; b < b1; b += L)
+            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(pp, s, KT, b, L, b1);
+    }
+    return bad;
+}
+
+template <int KT, int M, bool CHECK, class C, class Ptrs>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_split(
+    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, uint32_t* flag)
+{
+    static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one split item per workgroup, stripe order");
+    __shared__ SplitLds<C::SPLIT> lds;
+    const uint32_t c = blockIdx.x, s = blockIdx.z * kGridY + blockIdx.y;
+    if (s >= nstripes)
+        return;  // uniform: the ragged last z-slice
+    const bool bad = encode_item_split<KT, M, CHECK, C>(pp, s, c, len, cps, lds);
+    if constexpr (CHECK) {
+        if (bad)
+            atomicOr(flag, 1u);
+    }
+}
+
+// Vector i of every strip.  The surviving P rides on the last wave and the
+// surviving Q on the wave with the fewest data strips left, both folded into the
+// partial syndromes; after the barrier wave 0 writes the first rebuilt strip and
+// the last wave the second, each from the complete syndromes.  The plan's
+// constants come from scalar table reads placed between the issue of the strip
+// loads and their first use.
+template <int KT, int M, int SPLIT, int POL, bool BOUNDED, bool QS, class Ptrs>
+__device__ __forceinline__ void recover_split_vec(const Ptrs& pp, uint32_t s, RecPlan& pl,
+                                                  uint32_t w, uint32_t lane, uint32_t i,
+                                                  uint32_t nvec, SplitLds<SPLIT>& lds)
+{
+    using MW = Mem<u32x4>;
+    static_assert(SPLIT == 2 || SPLIT == 4, "every wave finishes 16 / SPLIT bytes per lane");
+    constexpr int KW = (KT + SPLIT - 1) / SPLIT;
+    constexpr int REM = SPLIT * KW - KT;  // strip slots the last wave leaves empty
+    constexpr uint32_t WP = SPLIT - 1, WQ = REM >= 2 ? SPLIT - 1 : SPLIT - 2;
+    const bool ok = !BOUNDED || i < nvec;
+    const uint8_t* pP = pp.get(s, KT);
+    const uint8_t* pQ = (M == 2) ? pp.get(s, KT + 1) : pP;
+    // fetched before the barrier, while a table read can still be a scalar load
+    const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
+    const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
+    const int x = pl.x, y = pl.y, nd = pl.nd;
+    const uint32_t lost = pl.lost;
+    const bool lostP = pl.lostP, lostQ = pl.lostQ;
+    const bool haveP = !lostP, haveQ = M == 2 && pl.needq && !lostQ;  // wave-uniform
+    const PartRec part = wave_case<0, SPLIT>(w, [=, &pp](auto wc) __attribute__((always_inline)) {
+        constexpr uint32_t W = decltype(wc)::value;
+        constexpr int J0 = static_cast<int>(W) * KW;
+        u32x4 pv = 0, qv = 0, d[KW];
+        if (W == WP && haveP && ok)
+            pv = MW::template ld<POL>(pP, i);
+        if (W == WQ && haveQ && ok)
+            qv = MW::template ld<POL>(pQ, i);
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j) {
+            const int jj = J0 + j;
+            const bool live = jj < KT && !((lost >> jj) & 1u);
+            d[j] = 0;
+            if (live && ok)
+                d[j] = MW::template ld<POL>(pp.get(s, jj), i);
+        }
+        const PlanMul mul = plan_constants_scalar(nd, x, y, lostP, lostQ);
+        u32x4 ps = 0, qs = 0;
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j) {
+            ps ^= d[j];
+            if constexpr (M == 2 && QS)
+                qs = gf_mul2(qs) ^ d[j];
+        }
+        if constexpr (M == 2 && QS && J0 != 0)
+            qs = gf_mulc(make_mul_table(gf_exp2_const(J0)), qs);
+        return PartRec{ps ^ pv, qs ^ qv, mul};
+    });
+    pl.t1 = part.mul.t1;
+    pl.t2 = part.mul.t2;
+    lds.p[w][lane] = part.p;
+    if constexpr (M == 2 && QS)
+        lds.q[w][lane] = part.q;
+    __syncthreads();
+    // Every wave finishes a quarter (half, for two waves) of the item: lane l of
+    // wave w owns ND consecutive dwords of the item's 256.  The work after the
+    // barrier -- LDS sums, two constant multiplications, the stores -- is what an
+    // item adds to its memory latency; spread over all waves it is ND/4 of what
+    // two writer waves would each do on whole 16-byte vectors.
+    constexpr int ND = 4 / SPLIT;
+    const uint32_t t = (w * 64u + lane) * ND;
+    const uint32_t ob = ((i - lane) << 4) + t * 4u;  // byte offset in the strip
+    const bool okw = !BOUNDED || ob < (nvec << 4);
+    const uint32_t* lp = reinterpret_cast<const uint32_t*>(lds.p);
+    const uint32_t* lq = reinterpret_cast<const uint32_t*>(lds.q);
+    uint32_t pt[ND], qt[ND];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+        pt[n] = lp[t + n];
+        qt[n] = 0;
+#pragma unroll
+        for (int u = 1; u < SPLIT; ++u)
+            pt[n] ^= lp[u * 256 + t + n];
+        if constexpr (M == 2 && QS) {
+            qt[n] = lq[t + n];
+#pragma unroll
+            for (int u = 1; u < SPLIT; ++u)
+                qt[n] ^= lq[u * 256 + t + n];
+        }
+    }
+    if (!okw)
+        return;
+    uint32_t o1[ND], o2[ND];
+    if (pl.nd == 0) {
+        if (pl.lostP)
+            st_words<POL, ND>(pP, ob, pt);
+        if (M == 2 && pl.lostQ)
+            st_words<POL, ND>(pQ, ob, qt);
+    } else if (pl.nd == 1) {
+        if (!pl.lostP) {
+            st_words<POL, ND>(pX, ob, pt);
+            if (M == 2 && pl.lostQ) {
+#pragma unroll
+                for (int n = 0; n < ND; ++n)
+                    o2[n] = qt[n] ^ gf_mulc(pl.t1, pt[n]);
+                st_words<POL, ND>(pQ, ob, o2);
+            }
+        } else {
+#pragma unroll
+            for (int n = 0; n < ND; ++n) {
+                o1[n] = gf_mulc(pl.t1, qt[n]);
+                o2[n] = pt[n] ^ o1[n];
+            }
+            st_words<POL, ND>(pX, ob, o1);
+            st_words<POL, ND>(pP, ob, o2);
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+            o1[n] = gf_mulc(pl.t1, pt[n]) ^ gf_mulc(pl.t2, qt[n]);
+            o2[n] = pt[n] ^ o1[n];
+        }
+        st_words<POL, ND>(pX, ob, o1);
+        st_words<POL, ND>(pY, ob, o2);
+    }
+}
+
+template <int KT, int M, class C, class Ptrs>
+__device__ __forceinline__ void reconstruct_item_split(const Ptrs& pp, uint32_t s, uint32_t c,
+                                                       uint32_t len, uint32_t cps, RecPlan& pl,
+                                                       bool aligned, SplitLds<C::SPLIT>& lds)
+{
+    constexpr int SPLIT = C::SPLIT, POL = C::POL;
+    constexpr uint32_t L = 64;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t nvec = len >> 4;
+    auto none = [](RecPlan&) {};
+    if (aligned) {
+        const uint32_t i = c * L + lane;
+        if ((c + 1) * L <= nvec) {
+            if (M == 2 && !pl.needq)  // wave-uniform
+                recover_split_vec<KT, M, SPLIT, POL, false, false>(pp, s, pl, w, lane, i, nvec,
+                                                                   lds);
+            else
+                recover_split_vec<KT, M, SPLIT, POL, false, true>(pp, s, pl, w, lane, i, nvec,
+                                                                  lds);
+        } else {
+            recover_split_vec<KT, M, SPLIT, POL, true, true>(pp, s, pl, w, lane, i, nvec, lds);
+        }
+        // recover_split_vec left the plan's constants in pl
+        const uint32_t tail = len & 15u;
+        if (w == 0 && tail && c == cps - 1 && lane < tail)
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, nvec * 16 + lane,
+                                                                   L, len, none);
+    } else if (w == 0) {
+        const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
+        pl.t1 = mul.t1;
+        pl.t2 = mul.t2;
+        const uint32_t b1 = min(len, (c + 1) * L * 16);
+        for (uint32_t b = c * L * 16 + lane; b < b1; b += L)
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, b, L, b1, none);
+    }
+}
+
+template <int KT, int M, class C, class Ptrs>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_split(
+    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, const uint8_t* fail, uint32_t f01,
+    uint32_t* bad)
+{
+    static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one split item per workgroup, stripe order");
+    __shared__ SplitLds<C::SPLIT> lds;
+    const uint32_t c = blockIdx.x, s = blockIdx.z * kGridY + blockIdx.y;
+    if (s >= nstripes)
+        return;  // uniform: the ragged last z-slice
+    // The pointer row and the failure pair are independent scalar reads: both are
+    // issued before either is used, so an item pays one memory round trip for
+    // them, not two, before its strip loads can go out.
+    const bool aligned = stripe_aligned<KT, M>(pp, s, KT);
+    uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
+    if (fail) {
+        const uint32_t f = load_fail_pair(fail, s);
+        f0 = f & 0xffu;
+        f1 = f >> 8;
+    }
+    RecPlan pl = decode_failures_mask<KT, M>(f0, f1);
+    const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
+    if (!pl.skip)  // uniform across the workgroup
+        reconstruct_item_split<KT, M, C>(pp, s, c, len, cps, pl, aligned, lds);
+    if (count_bad)  // after the item: nothing may be stored ahead of its pointer reads
+        atomicAdd(bad, 1u);
 }
 
 // ------------------------------------------------------------ segment work lists
@@ -834,7 +1355,7 @@ static inline uint32_t chunks_per_stripe(uint64_t len, int nthr, int U)
 template <class C>
 static bool grid_for(uint64_t len, uint32_t nstripes, uint32_t& cps, uint32_t& grid)
 {
-    cps = chunks_per_stripe(len, C::NTHR, C::U);
+    cps = chunks_per_stripe(len, C::ITEM, C::U);
     const uint64_t items = static_cast<uint64_t>(cps) * nstripes;
     if (items > 0x7fffffffull || len > kMaxStripLen)
         return false;
@@ -847,6 +1368,12 @@ static bool grid_for(uint64_t len, uint32_t nstripes, uint32_t& cps, uint32_t& g
     return true;
 }
 
+static inline dim3 split_grid(uint32_t cps, uint32_t nstripes)
+{
+    const uint32_t ny = nstripes < kGridY ? nstripes : kGridY;
+    return dim3(cps, ny, (nstripes + kGridY - 1) / kGridY);
+}
+
 template <int KT, int M, bool CHECK, class C, class Ptrs>
 static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
                             uint32_t* flag, hipStream_t st)
@@ -856,8 +1383,13 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
         return hipSuccess;
     if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp, k,
-                       static_cast<uint32_t>(len), cps, nstripes, flag);
+    if constexpr (C::SPLIT > 1)
+        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), split_grid(cps, nstripes),
+                           dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
+                           flag);
+    else
+        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp,
+                           k, static_cast<uint32_t>(len), cps, nstripes, flag);
     return hipGetLastError();
 }
 
@@ -870,8 +1402,13 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
         return hipSuccess;
     if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp, k,
-                       static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
+    if constexpr (C::SPLIT > 1)
+        hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), split_grid(cps, nstripes),
+                           dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
+                           fail, f01, bad);
+    else
+        hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp,
+                           k, static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
     return hipGetLastError();
 }
 
@@ -925,15 +1462,51 @@ constexpr int rec_waves_big(int k)
 {
     return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES : (k == 7 || k == 8) ? 4 : rec_waves(k);
 }
-template <int U, int MAP = 0, int WAVES = 0>
-using EncCfg = Cfg<kLanes, U, pol_aux(2, 18), MAP, 0, WAVES>;
+// Waves sharing one item (Cfg::SPLIT) in the batched kernels, and the waves per
+// SIMD that go with it, from same-box A/B runs of whole library builds
+// (tools/build_variants.sh + tools/gpu_lib_ab_shapes.sh, profiles/r02/split/;
+// microseconds per launch, split vs one wave per item):
+//   encode       8+2 x 64 KiB 387.7 vs 404 (4 waves share, 7 per SIMD; 6 -> 397),
+//                8+2 x 128 KiB 390 vs 404, 8+1 362 vs 380, 10+2 467 vs 496,
+//                12+2 279 vs 297, 14+2 326 vs 358, 16+2 x 256 KiB 380 vs 412;
+//                k = 5..7 two waves (7+2: 361 vs 365; four waves 379), k <= 4 one.
+//   reconstruct  pays more per wave for the split (failure decode and plan in every
+//                wave, the scaling of the Q parts): 16+2 x 256 KiB dual 380 vs 399 and
+//                16+2 x 64 KiB 382 vs 393 win at 8 waves per SIMD, 14+2 (349 vs 341),
+//                12+2 (330 vs 305) and 8+2 dual (447 vs 420) lose, so only k >= 16
+//                splits.  (A single-failure rebuild would win at 8+2, 362 vs 390,
+//                but the failure pattern is per-stripe data the launch cannot see.)
+// DRAID_ENC_SPLIT / DRAID_REC_SPLIT (>= 1) override every k, for sweeps only.
+#ifndef DRAID_ENC_SPLIT
+#define DRAID_ENC_SPLIT 0
+#endif
+#ifndef DRAID_REC_SPLIT
+#define DRAID_REC_SPLIT 0
+#endif
+constexpr int enc_split(int k) { return DRAID_ENC_SPLIT >= 1 ? DRAID_ENC_SPLIT : k <= 4 ? 1 : k <= 7 ? 2 : 4; }
+constexpr int rec_split(int k) { return DRAID_REC_SPLIT >= 1 ? DRAID_REC_SPLIT : k >= 16 ? 4 : 1; }
+constexpr int enc_split_waves(int k, int m)
+{
+    return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES
+           : enc_split(k) == 1  ? enc_waves(k)
+           : (k == 8 && m == 2) ? 7
+                                : 6;
+}
+constexpr int rec_split_waves(int k, bool big)
+{
+    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
+           : rec_split(k) == 1  ? (big ? rec_waves_big(k) : rec_waves(k))
+                                : 8;
+}
+template <int U, int MAP = 0, int WAVES = 0, int SPLIT = 1>
+using EncCfg = Cfg<kLanes * SPLIT, U, pol_aux(2, 18), MAP, 0, WAVES, SPLIT>;
 // Item order of the batched encode: XCD-aware (each XCD a contiguous run of
 // stripes) from k = 16 up -- 16+2 x 256 KiB encode 5988 vs 5747 GB/s (+4.2%,
 // lab variant 38 vs 0, median of 5 rounds, profiles/r01/cachepol/xcd_*.json) -- while it
 // costs 2-3% at 4+1 / 8+2 x 64 and 128 KiB, so the smaller k keep stripe order.
-constexpr int enc_map(int k) { return k >= 16 ? 3 : 0; }
-template <int U, int WAVES = 0>
-using RecCfg = Cfg<kLanes, U, pol_aux(-1, 18), 0, 0, WAVES>;
+constexpr int enc_map(int k) { return k >= 16 && enc_split(k) == 1 ? 3 : 0; }
+template <int U, int WAVES = 0, int SPLIT = 1>
+using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(-1, 18), 0, 0, WAVES, SPLIT>;
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 
@@ -947,7 +1520,8 @@ static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint
     switch (k) {
 #define DRAID_CASE(K) \
     case K:           \
-        return go_encode<K, M, false, EncCfg<enc_unroll(K), enc_map(K), enc_waves(K)>>(         \
+        return go_encode<K, M, false,                                                           \
+                         EncCfg<enc_unroll(K), enc_map(K), enc_split_waves(K, M), enc_split(K)>>(  \
             pp, k, len, nstripes, nullptr, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
@@ -965,9 +1539,11 @@ static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
 #define DRAID_CASE(K)                                                                       \
     case K:                                                                                 \
         return len >= kBigStrip                                                             \
-                   ? go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_waves_big(K)>>(         \
+                   ? go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_split_waves(K, true),   \
+                                                 rec_split(K)>>(                            \
                          pp, k, len, nstripes, fail, f01, bad, st)                          \
-                   : go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_waves(K)>>(             \
+                   : go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_split_waves(K, false),  \
+                                                 rec_split(K)>>(                            \
                          pp, k, len, nstripes, fail, f01, bad, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE

@@ -493,3 +493,68 @@ def test_full_size_linearity(ec, k, m, L, B):
         assert ec.encode(t.batch(ec), stream) == 0
     sync()
     assert torch.equal(x.strips()[:, k:], a.strips()[:, k:] ^ c.strips()[:, k:])
+
+
+# ------------------------------------------------------------ items shared by several waves
+
+SPLIT_K = [5, 6, 7, 8, 10, 12, 14, 16]   # stripe widths whose items are dealt over 2 or 4 waves
+
+
+@pytest.mark.parametrize("m", [1, 2])
+@pytest.mark.parametrize("k", SPLIT_K)
+def test_shared_items_every_length_class(ec, k, m):
+    """Whole chunks, a partial last chunk of 16-byte vectors, a byte tail, and a strip
+    shorter than one chunk: encode against the oracle, then every failure class
+    rebuilt, with the failure table at each alignment of its first byte (the kernel
+    reads it through aligned words)."""
+    stream = torch.cuda.current_stream().cuda_stream
+    for L, B in [(3 * 1024, 9), (2 * 1024 + 16 * 5, 7), (1024 + 16 * 3 + 7, 6), (48, 5), (5, 4)]:
+        rng = np.random.default_rng(k * 131 + m * 7 + L)
+        b = Batch(k, m, L, B, gap=16 + (-L) % 16, seed=k + L)   # every strip 16-byte aligned
+        assert b.table[0].item() % 16 == 0 and b.strip_stride % 16 == 0
+        before = host(b.strips())
+        assert ec.encode(b.batch(ec), stream) == 0
+        sync()
+        good = host(b.strips())
+        assert (good == oracle_encode(before, k, m)).all(), (k, m, L)
+        assert (host(b.view()[:, :, L:]) == 0).all()
+        for at in range(4):
+            fail = _random_failures(rng, B, k, m)
+            v = b.strips()
+            for s in range(B):
+                for f in fail[s]:
+                    if f != 0xFF:
+                        v[s, int(f)].fill_(0xA5)
+            holder = torch.zeros(2 * B + 8, dtype=torch.uint8, device=DEV)
+            base = (-holder.data_ptr()) % 4          # holder[base] is word aligned
+            tab = holder[base + at:base + at + 2 * B]
+            tab.copy_(dev(fail.reshape(-1)))
+            assert tab.data_ptr() % 4 == at
+            assert ec.reconstruct(b.batch(ec), tab, stream) == 0
+            sync()
+            assert (host(b.strips()) == good).all(), (k, m, L, at)
+            assert (host(b.view()[:, :, L:]) == 0).all()
+
+
+@pytest.mark.parametrize("k,m,L,B", [(8, 2, 64, 70000), (16, 2, 32, 66000), (4, 1, 64, 66000)])
+def test_more_stripes_than_one_grid_row(ec, k, m, L, B):
+    """More than 65535 stripes: the shared-item kernels index stripes through the
+    second and third grid dimensions."""
+    stream = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(B)
+    b = Batch(k, m, L, B, seed=B)
+    before = host(b.strips())
+    assert ec.encode(b.batch(ec), stream) == 0
+    sync()
+    good = host(b.strips())
+    assert (good == oracle_encode(before, k, m)).all()
+    fail = _random_failures(rng, B, k, m)
+    lost = torch.from_numpy(fail.astype(np.int64)).to(DEV)
+    v = b.strips()
+    rows = torch.arange(B, device=DEV)
+    for t in range(2):
+        sel = lost[:, t] != 0xFF
+        v[rows[sel], lost[sel, t]] = 0x5A
+    assert ec.reconstruct(b.batch(ec), dev(fail.reshape(-1)), stream) == 0
+    sync()
+    assert (host(b.strips()) == good).all()
