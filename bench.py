@@ -277,6 +277,9 @@ def run_single_process(args, torch, ec) -> None:
     print(json.dumps(out), flush=True)
 
 
+COMPILED_K = (2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16)  # widths with unrolled kernels
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -443,8 +446,13 @@ def main() -> None:
     pmc, pmc_src = load_pmc(workload)
 
     def roof(kind, gbs, nbytes):
-        name = (f"k_encode<K={k},M={m}> (draid_ec_encode)" if kind == "encode" else
-                f"k_reconstruct<K={k},M={m}> (draid_ec_reconstruct, {cfg['failures']} failure)")
+        # the kernel the library launches for this width (csrc/ec_kernels.hip,
+        # enc_split / rec_split): items shared by several waves from k = 5 (encode)
+        # and k = 16 (reconstruct) up
+        enc_k = "k_encode_split" if k >= 5 and k in COMPILED_K else "k_encode"
+        rec_k = "k_reconstruct_split" if k >= 16 and k in COMPILED_K else "k_reconstruct"
+        name = (f"{enc_k}<K={k},M={m}> (draid_ec_encode)" if kind == "encode" else
+                f"{rec_k}<K={k},M={m}> (draid_ec_reconstruct, {cfg['failures']} failure)")
         return {"bound": "hbm", "kernel": name, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                 "traffic": (pmc or {}).get(f"{kind}_hbm_bytes_per_launch"),

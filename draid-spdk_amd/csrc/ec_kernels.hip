@@ -41,19 +41,33 @@ int get_variant() { return g_variant; }
 
 // ------------------------------------------------------------ pointers
 
-struct TablePtrs {
+// AS4: read the table through the constant address space.  The table is input
+// only, and a constant-space read at a wave-uniform index is always a scalar load
+// (an ordinary global read becomes a per-lane load as soon as any store, atomic,
+// LDS write or barrier precedes it, and its pointer then lives in VGPRs).  The
+// split kernels and every reconstruct need that; the one-wave encode (k <= 4, the
+// check kernels) runs 2% faster on ordinary reads (4+1 x 64 KiB 203.2 vs 207.4
+// us), which the compiler already turns into scalar loads there.
+template <bool AS4>
+struct TablePtrsT {
     const uint8_t* const* tab;
     uint32_t stride;
-    // Read through the constant address space: the table is input only, and a
-    // constant-space read at a wave-uniform index is always a scalar load (an
-    // ordinary global read becomes a per-lane load as soon as any store, atomic,
-    // LDS write or barrier precedes it, and its pointer then lives in VGPRs).
     __device__ __forceinline__ const uint8_t* get(uint32_t s, int j) const
     {
-        typedef const uint8_t* const __attribute__((address_space(4)))* ctab;
-        return ((ctab)(uintptr_t)tab)[(size_t)s * stride + j];
+        if constexpr (AS4) {
+            typedef const uint8_t* const __attribute__((address_space(4)))* ctab;
+            return ((ctab)(uintptr_t)tab)[(size_t)s * stride + j];
+        } else {
+            return tab[(size_t)s * stride + j];
+        }
     }
 };
+#if defined(DRAID_TABLE_PLAIN)
+using TablePtrs = TablePtrsT<false>;
+#else
+using TablePtrs = TablePtrsT<true>;
+#endif
+using TablePlain = TablePtrsT<false>;
 
 // Regular layout: strip j of stripe s at base + s*stripe_stride + j*strip_stride
 // (a stripe cache laid out as one array, or pinned host stripes read in place).
@@ -750,9 +764,21 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
         item_coords<C>(b, cps, nstripes, s, c);
         uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
         if (fail) {
-            const uint32_t f = load_fail_pair(fail, s);
-            f0 = f & 0xffu;
-            f1 = f >> 8;
+            // The pair is read with byte (vector) loads for the P+Q widths 8..12 and
+            // through scalar word loads otherwise: measured, not derived -- same-box
+            // A/B of whole library builds (tools/gpu_lib_ab_shapes.sh, profiles/r02/
+            // split/fail_read_ab.jsonl), microseconds per launch, vector vs scalar:
+            // 8+2 x 64 KiB dual 409.8 vs 417.6, 10+2 497 vs 506, 12+2 301 vs 305; but
+            // 5+2 305 vs 288, 4+1 213 vs 203, 3+1 353 vs 328, 8+2 x 128 KiB single 385 vs
+            // 380, 14+2 347 vs 343.
+            if constexpr (M == 2 && KT >= 8 && KT <= 12) {
+                f0 = fail[2 * (size_t)s];
+                f1 = fail[2 * (size_t)s + 1];
+            } else {
+                const uint32_t f = load_fail_pair(fail, s);
+                f0 = f & 0xffu;
+                f1 = f >> 8;
+            }
         }
         RecPlan pl = decode_failures<M>(k, f0, f1);
         // A stripe that cannot be rebuilt is left untouched and counted once (by
@@ -772,6 +798,13 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
                 p.t1 = make_mul_table(0);
                 p.t2 = make_mul_table(0);
+            });
+        } else if constexpr (C::PLAN == 4) {
+            // constants from scalar reads of c_plan: no LDS, no barrier
+            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
+                const PlanMul mul = plan_constants_scalar(p.nd, p.x, p.y, p.lostP, p.lostQ);
+                p.t1 = mul.t1;
+                p.t2 = mul.t2;
             });
         } else if constexpr (C::PLAN == 1) {
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
@@ -1192,7 +1225,7 @@ struct WorkSrc {
 };
 
 template <int KT, int M, bool CHECK, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(TablePtrs pp, uint32_t k_rt, WorkSrc ws,
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(TablePlain pp, uint32_t k_rt, WorkSrc ws,
                                                          uint32_t nwork)
 {
     constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
@@ -1387,6 +1420,10 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
         hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), split_grid(cps, nstripes),
                            dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
                            flag);
+    else if constexpr (std::is_same<Ptrs, TablePtrs>::value)
+        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), 0,
+                           st, TablePlain{pp.tab, pp.stride}, k, static_cast<uint32_t>(len), cps,
+                           nstripes, flag);
     else
         hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp,
                            k, static_cast<uint32_t>(len), cps, nstripes, flag);
@@ -1505,8 +1542,14 @@ using EncCfg = Cfg<kLanes * SPLIT, U, pol_aux(2, 18), MAP, 0, WAVES, SPLIT>;
 // lab variant 38 vs 0, median of 5 rounds, profiles/r01/cachepol/xcd_*.json) -- while it
 // costs 2-3% at 4+1 / 8+2 x 64 and 128 KiB, so the smaller k keep stripe order.
 constexpr int enc_map(int k) { return k >= 16 && enc_split(k) == 1 ? 3 : 0; }
+// Plan constants of the one-wave reconstruct: 0 = exp/log tables staged in LDS
+// (production), 4 = scalar reads of c_plan as in the split kernel -- measured
+// slower there (8+2 x 64 KiB dual 425 vs 420 us, 12+2 310 vs 305), sweeps only.
+#ifndef DRAID_REC_PLAN
+#define DRAID_REC_PLAN 0
+#endif
 template <int U, int WAVES = 0, int SPLIT = 1>
-using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(-1, 18), 0, 0, WAVES, SPLIT>;
+using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(-1, 18), 0, DRAID_REC_PLAN, WAVES, SPLIT>;
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 
@@ -1749,7 +1792,7 @@ static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, const ui
     if (nwork == 0)
         return hipSuccess;
     hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                       TablePtrs{tab, k + M}, k, work_src<C>(seg_len, work, ulen), nwork);
+                       TablePlain{tab, k + M}, k, work_src<C>(seg_len, work, ulen), nwork);
     return hipGetLastError();
 }
 
