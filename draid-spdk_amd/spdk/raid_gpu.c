@@ -77,7 +77,8 @@ struct rg_info {
 	struct raid_bdev *raid_bdev;
 	struct draid_raid geom;
 	draid_stripe_cache *stripes;	/* per-stripe request queue, shared by the channels */
-	int ngpus;
+	int ngpus;			/* slots: contexts per channel, stripe s on slot s mod ngpus */
+	int ndevices;			/* GPUs the slots are dealt over */
 	struct raid_gpu_stats stats;
 };
 
@@ -816,7 +817,7 @@ rg_io_channel_resource_init(struct raid_bdev *raid_bdev, void *resource)
 	/* one context per GPU; stripe s runs on context s mod ngpus */
 	draid_ec_device_current(&dev);
 	for (g = 0; g < info->ngpus; g++) {
-		int rc = draid_ec_set_device(g);
+		int rc = draid_ec_set_device(g % info->ndevices);
 
 		if (rc == 0) {
 			rc = draid_ec_ctx_create(&ch->ctx[g]);
@@ -874,17 +875,21 @@ rg_start(struct raid_bdev *raid_bdev)
 		free(info);
 		return rc;
 	}
-	/* stripes spread over the node's GPUs by index (stripe mod G); DRAID_RAID_GPUS
-	 * caps G */
+	/* stripes spread over G slots by index (stripe mod G), one slot per GPU of the
+	 * node unless DRAID_RAID_GPUS sets G */
 	if (draid_ec_device_count(&count) != 0 || count < 1) {
 		SPDK_ERRLOG("no GPU: %s\n", draid_ec_last_error());
 		draid_stripe_cache_destroy(info->stripes);
 		free(info);
 		return -ENODEV;
 	}
-	info->ngpus = spdk_min(count, RG_MAX_GPUS);
+	info->ndevices = spdk_min(count, RG_MAX_GPUS);
+	info->ngpus = info->ndevices;
 	if (env && atoi(env) > 0) {
-		info->ngpus = spdk_min(info->ngpus, atoi(env));
+		/* fewer slots than GPUs leaves GPUs unused; more puts several slots on one
+		 * GPU (slot g on GPU g mod count), which is how the routing is exercised
+		 * on a one-GPU machine */
+		info->ngpus = spdk_min(atoi(env), RG_MAX_GPUS);
 	}
 
 	raid_bdev->bdev.blockcnt = info->geom.blockcnt;

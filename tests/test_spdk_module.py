@@ -55,12 +55,13 @@ def test_module_compiles_against_the_reference_headers_and_links_with_its_framew
         assert f" T {name}\n" in shim, name
 
 
-def run(binary, timeout=300):
+def run(binary, timeout=300, env=None):
     path = os.path.join(OUT, binary)
     if not os.access(path, os.X_OK):
         pytest.fail(f"{path} is missing: build it with `make -C tests/spdk` where the reference "
                     "tree is available (it ships to the GPU box prebuilt)")
-    p = subprocess.run([path], capture_output=True, text=True, timeout=timeout)
+    p = subprocess.run([path], capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **(env or {})))
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     return p.stdout
 
@@ -70,6 +71,15 @@ def test_raid6_module_under_the_reference_framework():
     out = run("spdk_raid_module_test")
     assert "ok raid6 n=10 strip=64KiB" in out and "ok raid5 n=5 strip=64KiB" in out
     assert "array checks passed" in out
+
+
+@pytest.mark.gpu
+def test_raid6_module_routes_stripes_over_several_device_slots():
+    """DRAID_RAID_GPUS=3 on a box with fewer GPUs puts several slots on one device:
+    one context per slot and channel, stripe s on slot s mod 3, every slot flushed and
+    polled by the channel's poller.  The same array checks must pass."""
+    out = run("spdk_raid_module_test", env={"DRAID_RAID_GPUS": "3"})
+    assert "ok raid6 n=10 strip=64KiB" in out and "array checks passed" in out
 
 
 @pytest.mark.gpu
