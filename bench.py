@@ -156,8 +156,11 @@ def cpu_baseline(k: int, m: int, S: int, failures: str, seconds: float, threads:
             "64-bit SWAR restatement of isa-l pq_gen_base + nibble-table gf_vect_mul, -O3 -mavx2")
     return {"value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "single_core_value": round(one, 3) if one else None,
-            "all_cores_value": round(allc, 3) if allc else None,
-            "all_cores": min(affinity, 512) if allc else None,
+            # every core this process may run on; when that is no more than `cores`
+            # (the GPU box gives a one-GPU job 16) the two runs are the same run
+            "all_cores_value": round(allc, 3) if allc else round(value, 3),
+            "all_cores": min(affinity, 512) if allc else threads,
+            "affinity_cores": affinity,
             "dram_resident_value": round(dram, 3) if dram else None,
             "dram_resident_sample": f"{B2} stripes ({(k + m) * S * B2 >> 20} MiB), {passes2} "
                                     f"passes in {el2:.1f}s, {threads} pthreads",
