@@ -561,7 +561,7 @@ int draid_ec_host_free(void* ptr)
 
 int draid_ec_host_register(void* ptr, size_t bytes)
 {
-    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped);
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
     return e == hipSuccess ? 0 : fail_hip(e, "hipHostRegister");
 }
 
