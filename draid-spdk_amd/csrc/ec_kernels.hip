@@ -1464,7 +1464,8 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
 // non-temporal buffer stores, aux sc1 nt: the line leaves L2 at once instead of
 // staying dirty until evicted):
 //   encode       non-temporal BUFFER loads (aux nt) -- lab variant 34
-//   reconstruct  non-temporal global loads          -- lab variant 26
+//   reconstruct  the same since the pointer table is read with scalar loads
+//                (DRAID_REC_LOAD_AUX below); before that, global nt loads
 // Measured inside bench.py against global nt loads + global nt stores
 // (tools/bench_ab.sh, lab variants, 2 interleaved rounds, profiles/r01/cachepol/):
 // encode 8+2 x 64 KiB 6529 vs 6408 GB/s (+1.9%), 8+2 x 128 KiB +4.2%,
@@ -1548,8 +1549,17 @@ constexpr int enc_map(int k) { return k >= 16 && enc_split(k) == 1 ? 3 : 0; }
 #ifndef DRAID_REC_PLAN
 #define DRAID_REC_PLAN 0
 #endif
+// Reconstruct load policy: 2 = non-temporal buffer loads as in the encode
+// (production), -1 = non-temporal global loads.  Round 1 measured the global form
+// 1.8% faster at 8+2 x 64 KiB, when the pointer table came through per-lane loads
+// and every buffer access paid a readfirstlane loop; with the pointers in SGPRs
+// the buffer form wins by 0.5-1.1% at every width (8+2 x 64 KiB dual 405.5 vs
+// 410.0 us, 10+2 491 vs 495.5, 16+2 x 256 KiB 378.5 vs 380.7).
+#ifndef DRAID_REC_LOAD_AUX
+#define DRAID_REC_LOAD_AUX 2
+#endif
 template <int U, int WAVES = 0, int SPLIT = 1>
-using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(-1, 18), 0, DRAID_REC_PLAN, WAVES, SPLIT>;
+using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(DRAID_REC_LOAD_AUX, 18), 0, DRAID_REC_PLAN, WAVES, SPLIT>;
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 
