@@ -45,9 +45,10 @@ int get_variant() { return g_variant; }
 // only, and a constant-space read at a wave-uniform index is always a scalar load
 // (an ordinary global read becomes a per-lane load as soon as any store, atomic,
 // LDS write or barrier precedes it, and its pointer then lives in VGPRs).  The
-// split kernels and every reconstruct need that; the one-wave encode (k <= 4, the
-// check kernels) runs 2% faster on ordinary reads (4+1 x 64 KiB 203.2 vs 207.4
-// us), which the compiler already turns into scalar loads there.
+// split kernels and every reconstruct need that; the one-wave encode (k = 2, the
+// runtime-k fallback, the check kernels) ran 2% faster on ordinary reads (4+1 x
+// 64 KiB 203.2 vs 207.4 us), which the compiler already turns into scalar loads
+// there.
 template <bool AS4>
 struct TablePtrsT {
     const uint8_t* const* tab;
@@ -1507,7 +1508,8 @@ constexpr int rec_waves_big(int k)
 //   encode       8+2 x 64 KiB 387.7 vs 404 (4 waves share, 7 per SIMD; 6 -> 397),
 //                8+2 x 128 KiB 390 vs 404, 8+1 362 vs 380, 10+2 467 vs 496,
 //                12+2 279 vs 297, 14+2 326 vs 358, 16+2 x 256 KiB 380 vs 412;
-//                k = 5..7 two waves (7+2: 361 vs 365; four waves 379), k <= 4 one.
+//                k = 3..7 two waves (7+2: 361 vs 365, four waves 379; 4+1 194.7 vs 202.6
+//                at 5 per SIMD; 3+1 310.6 vs 318.2; 4+2 239.5 vs 242.3), k = 2 one.
 //   reconstruct  pays more per wave for the split (failure decode and plan in every
 //                wave, the scaling of the Q parts): 16+2 x 256 KiB dual 380 vs 399 and
 //                16+2 x 64 KiB 382 vs 393 win at 8 waves per SIMD, 14+2 (349 vs 341),
@@ -1521,13 +1523,14 @@ constexpr int rec_waves_big(int k)
 #ifndef DRAID_REC_SPLIT
 #define DRAID_REC_SPLIT 0
 #endif
-constexpr int enc_split(int k) { return DRAID_ENC_SPLIT >= 1 ? DRAID_ENC_SPLIT : k <= 4 ? 1 : k <= 7 ? 2 : 4; }
+constexpr int enc_split(int k) { return DRAID_ENC_SPLIT >= 1 ? DRAID_ENC_SPLIT : k <= 2 ? 1 : k <= 7 ? 2 : 4; }
 constexpr int rec_split(int k) { return DRAID_REC_SPLIT >= 1 ? DRAID_REC_SPLIT : k >= 16 ? 4 : 1; }
 constexpr int enc_split_waves(int k, int m)
 {
     return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES
            : enc_split(k) == 1  ? enc_waves(k)
            : (k == 8 && m == 2) ? 7
+           : (m == 1 && (k == 4 || k == 5)) ? 5
                                 : 6;
 }
 constexpr int rec_split_waves(int k, bool big)
