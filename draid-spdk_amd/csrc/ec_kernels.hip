@@ -1238,6 +1238,19 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(T
     }
 }
 
+// The shared-item encode over a segment list: one workgroup per work item.
+template <int KT, int M, class C>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work_split(
+    TablePtrs pp, WorkSrc ws, uint32_t nwork)
+{
+    static_assert(KT > 0 && C::SPLIT > 1, "shared items need a compile-time width");
+    constexpr uint32_t CB = static_cast<uint32_t>(C::ITEM) * C::U * 16;
+    __shared__ SplitLds<C::SPLIT> lds;
+    uint32_t seg, chunk, len, cps;
+    ws.get(blockIdx.x, CB, seg, chunk, len, cps);
+    encode_item_split<KT, M, false, C>(pp, seg, chunk, len, cps, lds);
+}
+
 template <int KT, int M, class C>
 __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
                                                               WorkSrc ws, const uint8_t* fail,
@@ -1791,7 +1804,7 @@ hipError_t launch_check(uint32_t k, uint32_t m, uint64_t len, const uint8_t* con
 template <class C>
 static WorkSrc work_src(const uint32_t* seg_len, const void* work, uint32_t ulen)
 {
-    constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
+    constexpr uint32_t CB = static_cast<uint32_t>(C::ITEM) * C::U * 16;
     WorkSrc ws{static_cast<const WorkItem*>(work), seg_len, ulen, 1};
     if (!work)
         ws.ucps = ulen ? (ulen + CB - 1) / CB : 1;
@@ -1804,8 +1817,12 @@ static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, const ui
 {
     if (nwork == 0)
         return hipSuccess;
-    hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                       TablePlain{tab, k + M}, k, work_src<C>(seg_len, work, ulen), nwork);
+    if constexpr (C::SPLIT > 1)
+        hipLaunchKernelGGL((k_encode_work_split<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                           TablePtrs{tab, k + M}, work_src<C>(seg_len, work, ulen), nwork);
+    else
+        hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                           TablePlain{tab, k + M}, k, work_src<C>(seg_len, work, ulen), nwork);
     return hipGetLastError();
 }
 
@@ -1848,9 +1865,11 @@ hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* tabl
     switch (k) {
 #define DRAID_CASE(K)                                                                        \
     case K:                                                                                  \
-        return m == 1 ? go_encode_work<K, 1, EncCfg<enc_unroll(K), 0, enc_waves(K)>>(        \
+        return m == 1 ? go_encode_work<K, 1, EncCfg<enc_unroll(K), 0, enc_split_waves(K, 1),  \
+                                                    enc_split(K)>>(                          \
                             table, k, seg_len, work, ulen, nwork, st)                        \
-                      : go_encode_work<K, 2, EncCfg<enc_unroll(K), 0, enc_waves(K)>>(        \
+                      : go_encode_work<K, 2, EncCfg<enc_unroll(K), 0, enc_split_waves(K, 2),  \
+                                                    enc_split(K)>>(                          \
                             table, k, seg_len, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
