@@ -111,6 +111,15 @@ constexpr int pol_aux(int load_aux, int store_aux)
     return 3 | ((load_aux + 1) << 8) | ((store_aux + 1) << 16);
 }
 
+// 1: the shared-item reconstruct loads a strip it skips (lost, or not needed)
+// through a descriptor with no records instead of branching around the load
+// (Mem<u32x4>::ld_if): 16+2 x 256 KiB dual 380 vs 389 us.  The one-wave
+// reconstruct keeps its uniform branches -- there the same change is neutral to
+// 1% slower (8+2 x 128 KiB single 377.6 vs 374.1, 4+1 207.6 vs 204.0).  0 for A/B.
+#ifndef DRAID_DEAD_LOADS
+#define DRAID_DEAD_LOADS 1
+#endif
+
 template <class W>
 struct Mem;
 
@@ -134,6 +143,22 @@ struct Mem<u32x4> {
             return __builtin_nontemporal_load(q);
         else
             return *q;
+    }
+    // Loads vector i when `live` (wave-uniform), zeros otherwise.  Through a buffer
+    // descriptor a dead load is one with no records -- it returns zeros without
+    // touching memory -- so a skipped strip costs neither a branch nor the moves
+    // that zero its registers.
+    template <int POL>
+    static __device__ __forceinline__ u32x4 ld_if(const uint8_t* p, uint32_t i, bool live)
+    {
+        constexpr int aux = (POL >> 8) & 0xff;
+        if constexpr (aux != 0 && DRAID_DEAD_LOADS) {
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t*>(p), 0, live ? 0x7fffffff : 0, 0x00020000);
+            return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(i << 4), 0, aux - 1);
+        } else {
+            return live ? ld<POL>(p, i) : u32x4(0);
+        }
     }
     template <int POL>
     static __device__ __forceinline__ void st(const uint8_t* p, uint32_t i, u32x4 v)
@@ -159,6 +184,11 @@ struct Mem<uint32_t> {
     static __device__ __forceinline__ uint32_t ld(const uint8_t* p, uint32_t i)
     {
         return *((gcb)p + i);
+    }
+    template <int POL>
+    static __device__ __forceinline__ uint32_t ld_if(const uint8_t* p, uint32_t i, bool live)
+    {
+        return live ? ld<POL>(p, i) : 0u;
     }
     template <int POL>
     static __device__ __forceinline__ void st(const uint8_t* p, uint32_t i, uint32_t v)
@@ -1031,17 +1061,17 @@ __device__ __forceinline__ void recover_split_vec(const Ptrs& pp, uint32_t s, Re
         constexpr uint32_t W = decltype(wc)::value;
         constexpr int J0 = static_cast<int>(W) * KW;
         u32x4 pv = 0, qv = 0, d[KW];
-        if (W == WP && haveP && ok)
-            pv = MW::template ld<POL>(pP, i);
-        if (W == WQ && haveQ && ok)
-            qv = MW::template ld<POL>(pQ, i);
+        if constexpr (W == WP)
+            pv = ok ? MW::template ld_if<POL>(pP, i, haveP) : u32x4(0);
+        if constexpr (W == WQ)
+            qv = ok ? MW::template ld_if<POL>(pQ, i, haveQ) : u32x4(0);
 #pragma unroll
         for (int j = KW - 1; j >= 0; --j) {
             const int jj = J0 + j;
-            const bool live = jj < KT && !((lost >> jj) & 1u);
             d[j] = 0;
-            if (live && ok)
-                d[j] = MW::template ld<POL>(pp.get(s, jj), i);
+            if (jj < KT)  // compile-time once unrolled: a ragged last wave has fewer strips
+                d[j] = ok ? MW::template ld_if<POL>(pp.get(s, jj), i, !((lost >> jj) & 1u))
+                          : u32x4(0);
         }
         const PlanMul mul = plan_constants_scalar(nd, x, y, lostP, lostQ);
         u32x4 ps = 0, qs = 0;
