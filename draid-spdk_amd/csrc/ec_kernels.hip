@@ -49,6 +49,9 @@ int get_variant() { return g_variant; }
 // runtime-k fallback, the check kernels) ran 2% faster on ordinary reads (4+1 x
 // 64 KiB 203.2 vs 207.4 us), which the compiler already turns into scalar loads
 // there.
+#ifndef DRAID_KEEP_POINTERS
+#define DRAID_KEEP_POINTERS 1
+#endif
 template <bool AS4>
 struct TablePtrsT {
     const uint8_t* const* tab;
@@ -57,7 +60,15 @@ struct TablePtrsT {
     {
         if constexpr (AS4) {
             typedef const uint8_t* const __attribute__((address_space(4)))* ctab;
-            return ((ctab)(uintptr_t)tab)[(size_t)s * stride + j];
+            const uint8_t* p = ((ctab)(uintptr_t)tab)[(size_t)s * stride + j];
+#if DRAID_KEEP_POINTERS
+            // Opaque to the register allocator: a constant-space load is trivially
+            // rematerialisable, and under SGPR pressure the compiler re-read the whole
+            // pointer row (s_load_dwordx16 + wait) in front of EVERY strip load of
+            // the one-wave reconstruct, serialising the loads behind scalar round trips.
+            asm("" : "+s"(p));
+#endif
+            return p;
         } else {
             return tab[(size_t)s * stride + j];
         }
