@@ -1528,16 +1528,19 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
 // (6496 vs 6500), 128 KiB +0.8%, 16+2 +0.3%, 4+1 -0.4%.  Buffer loads in the
 // reconstruct lose 1.8% at 8+2 x 64 KiB (they win 1-2% at 128/256 KiB).
 constexpr int kLanes = 64;
-// Waves per SIMD each kernel is built for (Cfg::WAVES), from a sweep of every
-// setting over the stripe shapes (tools/gpu_shape_matrix.sh, same-box A/B of whole
-// library builds, profiles/r02/occupancy/): the best count falls as a wave's
-// loads in flight grow with k.  Microseconds per 4096-stripe launch, best vs the
-// compiler's own choice:
-//   encode       8+2 x 64 KiB 403.8 vs 411.5 (6 waves), 8+2 x 128 KiB 804.7 vs 850.7,
-//                10+2 498.8 vs 508.1, 16+2 x 256 KiB 402.4 vs 410.2, 4+1 203.7 vs 205.2 (7)
-//   reconstruct  8+2 x 64 KiB dual 411 vs 420 (5; 4 -> 417), 8+2 x 128 KiB 822.8 vs 858.0
-//                (4; 5 -> 837.6), 10+2 498.3 vs 509.4 (4), 16+2 x 256 KiB 399.2 vs 408.6 (3),
-//                4+1 and 6+2: the compiler's choice (7-8 waves) is already best.
+// Waves per SIMD each one-wave kernel is built for (Cfg::WAVES), from sweeps of
+// every setting over the stripe shapes (same-box A/B of whole library builds:
+// tools/gpu_shape_matrix.sh, profiles/r02/occupancy/; redone for the reconstruct
+// after its loads and pointer reads changed, tools/gpu_lib_ab_shapes.sh,
+// profiles/r02/occupancy/rec_waves_final.jsonl): the best count falls as a
+// wave's loads in flight grow with k.  Microseconds per launch of 2.1-2.7 GB:
+//   encode       (k = 2 and the segment lists; wider stripes share items, below)
+//                8+2 x 64 KiB 403.8 vs 411.5 the compiler's choice (6 waves), 4+1 203.7 vs 205.2 (7)
+//   reconstruct  8+2 dual 401.4 at 4 waves (5: 408.1, 3: 441, 6: 414), 7+2 359.6 vs
+//                364.5 (4 vs 5), 8+1 375.3 vs 385.1, 6+1 284.4 at 4 (5: 290.4, the
+//                compiler's: 295.5), 6+2 321.6 at 5 (4: 334, 6: 326.7), 5+2 283.5 at 6
+//                (5: 297, compiler's: 289), 10+2 492 and 12+2 298 at 4 (3: 500 / 307,
+//                5: 503 / 305), 14+2 339 at 3 (4: 351); k <= 4: the compiler's choice.
 // DRAID_ENC_WAVES / DRAID_REC_WAVES (>= 0) override every k, for such sweeps only.
 #ifndef DRAID_ENC_WAVES
 #define DRAID_ENC_WAVES -1
@@ -1545,15 +1548,15 @@ constexpr int kLanes = 64;
 #ifndef DRAID_REC_WAVES
 #define DRAID_REC_WAVES -1
 #endif
-constexpr uint64_t kBigStrip = 128u << 10;  // strips from here on use the *_big counts
 constexpr int enc_waves(int k) { return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES : k <= 4 ? 7 : 6; }
-constexpr int rec_waves(int k)
+constexpr int rec_waves(int k, int m)
 {
-    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES : k <= 6 ? 0 : k <= 8 ? 5 : k <= 12 ? 4 : 3;
-}
-constexpr int rec_waves_big(int k)
-{
-    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES : (k == 7 || k == 8) ? 4 : rec_waves(k);
+    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
+           : k <= 4             ? 0
+           : k == 5             ? (m == 2 ? 6 : 5)
+           : k == 6             ? (m == 2 ? 5 : 4)
+           : k <= 12            ? 4
+                                : 3;
 }
 // Waves sharing one item (Cfg::SPLIT) in the batched kernels, and the waves per
 // SIMD that go with it, from same-box A/B runs of whole library builds
@@ -1587,11 +1590,9 @@ constexpr int enc_split_waves(int k, int m)
            : (m == 1 && (k == 4 || k == 5)) ? 5
                                 : 6;
 }
-constexpr int rec_split_waves(int k, bool big)
+constexpr int rec_split_waves(int k, int m)
 {
-    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
-           : rec_split(k) == 1  ? (big ? rec_waves_big(k) : rec_waves(k))
-                                : 8;
+    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES : rec_split(k) == 1 ? rec_waves(k, m) : 8;
 }
 template <int U, int MAP = 0, int WAVES = 0, int SPLIT = 1>
 using EncCfg = Cfg<kLanes * SPLIT, U, pol_aux(2, 18), MAP, 0, WAVES, SPLIT>;
@@ -1648,13 +1649,9 @@ static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
     switch (k) {
 #define DRAID_CASE(K)                                                                       \
     case K:                                                                                 \
-        return len >= kBigStrip                                                             \
-                   ? go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_split_waves(K, true),   \
-                                                 rec_split(K)>>(                            \
-                         pp, k, len, nstripes, fail, f01, bad, st)                          \
-                   : go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_split_waves(K, false),  \
-                                                 rec_split(K)>>(                            \
-                         pp, k, len, nstripes, fail, f01, bad, st);
+        return go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_split_waves(K, M),            \
+                                           rec_split(K)>>(pp, k, len, nstripes, fail, f01,  \
+                                                          bad, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
@@ -1929,9 +1926,9 @@ hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const*
     switch (k) {
 #define DRAID_CASE(K)                                                                         \
     case K:                                                                                   \
-        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K), rec_waves(K)>>(       \
+        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K), rec_waves(K, 1)>>(    \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st) \
-                      : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K), rec_waves(K)>>(       \
+                      : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K), rec_waves(K, 2)>>(    \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
