@@ -83,6 +83,25 @@ def test_raid6_module_routes_stripes_over_several_device_slots():
 
 
 @pytest.mark.gpu
+def test_module_sustains_queue_depth_32():
+    """The bdevperf-shaped harness (full-stripe writes, strip writes, healthy and degraded
+    reads with 32 requests outstanding on one reactor): every request completes, none fails,
+    and the poller batches several requests into each launch."""
+    import json
+    path = os.path.join(OUT, "spdk_raid_module_bench")
+    if not os.access(path, os.X_OK):
+        pytest.fail(f"{path} is missing: build it with `make -C tests/spdk`")
+    p = subprocess.run([path, "6", "10", "64", "32", "0.3"], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    rows = [json.loads(line) for line in p.stdout.splitlines() if line.startswith("{")]
+    assert [r["job"] for r in rows] == ["full_stripe_write", "strip_write_rmw", "full_stripe_read",
+                                        "full_stripe_read_1_degraded", "full_stripe_read_2_degraded"]
+    assert all(r["failed"] == 0 and r["ios"] > 100 for r in rows)
+    assert rows[0]["requests_per_launch"] > 2 and rows[4]["launches"] > 0
+
+
+@pytest.mark.gpu
 def test_reference_raid5_simple_calls_the_engine_at_its_xor_gen_call_site():
     out = run("spdk_raid5_simple_test")
     assert "stripe parities equal the known answer" in out
