@@ -451,9 +451,9 @@ def main() -> None:
     def roof(kind, gbs, nbytes):
         # the kernel the library launches for this width (csrc/ec_kernels.hip,
         # enc_split / rec_split): items shared by several waves from k = 3 (encode)
-        # and k = 16 (reconstruct) up
+        # and k = 8 (reconstruct) up
         enc_k = "k_encode_split" if k >= 3 and k in COMPILED_K else "k_encode"
-        rec_k = "k_reconstruct_split" if k >= 16 and k in COMPILED_K else "k_reconstruct"
+        rec_k = "k_reconstruct_cols" if k >= 8 and k in COMPILED_K else "k_reconstruct"
         name = (f"{enc_k}<K={k},M={m}> (draid_ec_encode)" if kind == "encode" else
                 f"{rec_k}<K={k},M={m}> (draid_ec_reconstruct, {cfg['failures']} failure)")
         return {"bound": "hbm", "kernel": name, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,

@@ -1230,6 +1230,186 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_s
         atomicAdd(bad, 1u);
 }
 
+// ---- loads dealt by strip, arithmetic dealt by column
+//
+// The shared reconstruct above splits the ARITHMETIC by strip as well: every wave
+// runs a Horner chain over its strips on whole 16-byte vectors and its Q part then
+// needs a constant multiplication to line up (36 VALU per wave), which is what a
+// VALU-heavy dual-failure rebuild cannot afford (8+2: 580 VALU per item against
+// 435 for one wave).  Here only the LOADS are dealt by strip: each wave loads its
+// strips as 16-byte vectors and parks them in LDS untouched (one row per strip;
+// a strip that is lost or not needed arrives as zeros through a descriptor with no
+// records).  After one barrier every wave owns a quarter of the item's 256 dword
+// columns and runs the one Horner chain down all k strips of its columns: the
+// same arithmetic as the one-wave kernel, no scaling, spread evenly over the waves.
+template <int KT>
+struct ColLds {
+    u32x4 row[KT + 2][64];  // rows 0..KT-1 data strips, KT the surviving P, KT+1 the surviving Q
+};
+
+template <int KT, int M, int SPLIT, int POL, bool BOUNDED, bool QS, class Ptrs>
+__device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, RecPlan& pl,
+                                                 uint32_t w, uint32_t lane, uint32_t i,
+                                                 uint32_t nvec, ColLds<KT>& lds)
+{
+    using MW = Mem<u32x4>;
+    static_assert(SPLIT == 2 || SPLIT == 4, "every wave finishes 16 / SPLIT bytes per lane");
+    constexpr int KW = (KT + SPLIT - 1) / SPLIT;
+    constexpr int REM = SPLIT * KW - KT;
+    constexpr uint32_t WP = SPLIT - 1, WQ = REM >= 2 ? SPLIT - 1 : SPLIT - 2;
+    const bool ok = !BOUNDED || i < nvec;
+    const uint8_t* pP = pp.get(s, KT);
+    const uint8_t* pQ = (M == 2) ? pp.get(s, KT + 1) : pP;
+    const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
+    const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
+    const uint32_t lost = pl.lost;
+    const bool haveP = !pl.lostP, haveQ = M == 2 && QS && pl.needq && !pl.lostQ;
+    // phase 1: this wave's strips -> LDS rows (zeros for the ones it skips)
+    wave_case<0, SPLIT>(w, [=, &pp, &lds](auto wc) __attribute__((always_inline)) {
+        constexpr uint32_t W = decltype(wc)::value;
+        constexpr int J0 = static_cast<int>(W) * KW;
+        u32x4 d[KW], pv = 0, qv = 0;
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j) {
+            d[j] = 0;
+            if (J0 + j < KT)
+                d[j] = ok ? MW::template ld_if<POL>(pp.get(s, J0 + j), i, !((lost >> (J0 + j)) & 1u))
+                          : u32x4(0);
+        }
+        if constexpr (W == WP)
+            pv = ok ? MW::template ld_if<POL>(pP, i, haveP) : u32x4(0);
+        if constexpr (W == WQ)
+            qv = ok ? MW::template ld_if<POL>(pQ, i, haveQ) : u32x4(0);
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j)
+            if (J0 + j < KT)
+                lds.row[J0 + j][lane] = d[j];
+        if constexpr (W == WP)
+            lds.row[KT][lane] = pv;
+        if constexpr (W == WQ)
+            lds.row[KT + 1][lane] = qv;
+        return PartPQ{};
+    });
+    const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
+    pl.t1 = mul.t1;
+    pl.t2 = mul.t2;
+    __syncthreads();
+    // phase 2: this wave's columns, all strips
+    constexpr int ND = 4 / SPLIT;
+    const uint32_t t = (w * 64u + lane) * ND;
+    const uint32_t ob = ((i - lane) << 4) + t * 4u;
+    const bool okw = !BOUNDED || ob < (nvec << 4);
+    const uint32_t* L = reinterpret_cast<const uint32_t*>(lds.row);
+    uint32_t pt[ND], qt[ND];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+        pt[n] = 0;
+        qt[n] = 0;
+    }
+#pragma unroll
+    for (int j = KT - 1; j >= 0; --j) {
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+            const uint32_t d = L[j * 256 + t + n];
+            pt[n] ^= d;
+            if constexpr (M == 2 && QS)
+                qt[n] = gf_mul2(qt[n]) ^ d;
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+        pt[n] ^= L[KT * 256 + t + n];
+        if constexpr (M == 2 && QS)
+            qt[n] ^= L[(KT + 1) * 256 + t + n];
+    }
+    if (!okw)
+        return;
+    uint32_t o1[ND], o2[ND];
+    if (pl.nd == 0) {
+        if (pl.lostP)
+            st_words<POL, ND>(pP, ob, pt);
+        if (M == 2 && pl.lostQ)
+            st_words<POL, ND>(pQ, ob, qt);
+    } else if (pl.nd == 1) {
+        if (!pl.lostP) {
+            st_words<POL, ND>(pX, ob, pt);
+            if (M == 2 && pl.lostQ) {
+#pragma unroll
+                for (int n = 0; n < ND; ++n)
+                    o2[n] = qt[n] ^ gf_mulc(pl.t1, pt[n]);
+                st_words<POL, ND>(pQ, ob, o2);
+            }
+        } else {
+#pragma unroll
+            for (int n = 0; n < ND; ++n) {
+                o1[n] = gf_mulc(pl.t1, qt[n]);
+                o2[n] = pt[n] ^ o1[n];
+            }
+            st_words<POL, ND>(pX, ob, o1);
+            st_words<POL, ND>(pP, ob, o2);
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+            o1[n] = gf_mulc(pl.t1, pt[n]) ^ gf_mulc(pl.t2, qt[n]);
+            o2[n] = pt[n] ^ o1[n];
+        }
+        st_words<POL, ND>(pX, ob, o1);
+        st_words<POL, ND>(pY, ob, o2);
+    }
+}
+
+template <int KT, int M, class C, class Ptrs>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_cols(
+    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, const uint8_t* fail, uint32_t f01,
+    uint32_t* bad)
+{
+    static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one shared item per workgroup, stripe order");
+    constexpr int SPLIT = C::SPLIT, POL = C::POL;
+    __shared__ ColLds<KT> lds;
+    const uint32_t c = blockIdx.x, s = blockIdx.z * kGridY + blockIdx.y;
+    if (s >= nstripes)
+        return;
+    const bool aligned = stripe_aligned<KT, M>(pp, s, KT);
+    uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
+    if (fail) {
+        const uint32_t f = load_fail_pair(fail, s);
+        f0 = f & 0xffu;
+        f1 = f >> 8;
+    }
+    RecPlan pl = decode_failures_mask<KT, M>(f0, f1);
+    const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
+    if (!pl.skip) {
+        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+        const uint32_t nvec = len >> 4;
+        auto none = [](RecPlan&) {};
+        if (aligned) {
+            const uint32_t i = c * 64u + lane;
+            if ((c + 1) * 64u <= nvec) {
+                if (M == 2 && !pl.needq)
+                    recover_cols_vec<KT, M, SPLIT, POL, false, false>(pp, s, pl, w, lane, i, nvec, lds);
+                else
+                    recover_cols_vec<KT, M, SPLIT, POL, false, true>(pp, s, pl, w, lane, i, nvec, lds);
+            } else {
+                recover_cols_vec<KT, M, SPLIT, POL, true, true>(pp, s, pl, w, lane, i, nvec, lds);
+            }
+            const uint32_t tail = len & 15u;
+            if (w == 0 && tail && c == cps - 1 && lane < tail)
+                recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl,
+                                                                       nvec * 16 + lane, 64, len, none);
+        } else if (w == 0) {
+            const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
+            pl.t1 = mul.t1;
+            pl.t2 = mul.t2;
+            const uint32_t b1 = min(len, (c + 1) * 1024u);
+            for (uint32_t b = c * 1024u + lane; b < b1; b += 64)
+                recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, b, 64, b1, none);
+        }
+    }
+    if (count_bad)
+        atomicAdd(bad, 1u);
+}
+
 // ------------------------------------------------------------ segment work lists
 
 // Scatter-gather form (ec_ctx.cpp): a batch of variable-length segments, each
@@ -1494,7 +1674,11 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
         return hipSuccess;
     if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    if constexpr (C::SPLIT > 1)
+    if constexpr (C::SPLIT > 1 && C::PLAN == 5)
+        hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), split_grid(cps, nstripes),
+                           dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
+                           fail, f01, bad);
+    else if constexpr (C::SPLIT > 1)
         hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), split_grid(cps, nstripes),
                            dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
                            fail, f01, bad);
@@ -1567,13 +1751,25 @@ constexpr int rec_waves(int k, int m)
 //                12+2 279 vs 297, 14+2 326 vs 358, 16+2 x 256 KiB 380 vs 412;
 //                k = 3..7 two waves (7+2: 361 vs 365, four waves 379; 4+1 194.7 vs 202.6
 //                at 5 per SIMD; 3+1 310.6 vs 318.2; 4+2 239.5 vs 242.3), k = 2 one.
-//   reconstruct  pays more per wave for the split (failure decode and plan in every
-//                wave, the scaling of the Q parts): 16+2 x 256 KiB dual 380 vs 399 and
-//                16+2 x 64 KiB 382 vs 393 win at 8 waves per SIMD, 14+2 (349 vs 341),
-//                12+2 (330 vs 305) and 8+2 dual (447 vs 420) lose, so only k >= 16
-//                splits.  (A single-failure rebuild would win at 8+2, 362 vs 390,
-//                but the failure pattern is per-stripe data the launch cannot see.)
+//   reconstruct  dealing the arithmetic by strip as the encode does costs it too much
+//                (failure decode and plan in every wave, the scaling of the Q parts):
+//                with four waves only k = 16 wins (380 vs 399), 14+2 (349 vs 341),
+//                12+2 (330 vs 305) and 8+2 dual (447 vs 420) lose.  Dealing only the
+//                LOADS by strip and the arithmetic by column (k_reconstruct_cols), two
+//                waves per item, wins from k = 8 up against the one-wave kernel at its
+//                best occupancy: 8+1 365.6 vs 376.7, 10+2 480 vs 494, 12+2 288 vs 298.7,
+//                14+2 332 vs 341.5, 8+2 dual 400.5 vs 401.6-406.7, 16+2 x 256 KiB 381 vs
+//                381 (= four waves by strip); four waves lose below k = 16 (8+2 dual 478),
+//                k <= 7 stays one wave (6+2: 323 vs 322).
 // DRAID_ENC_SPLIT / DRAID_REC_SPLIT (>= 1) override every k, for sweeps only.
+// How a shared reconstruct item is divided (the one-wave kernel always stages the
+// exp/log tables in LDS): 5 = loads by strip, arithmetic by column (production,
+// k_reconstruct_cols), 0 = loads and arithmetic by strip (k_reconstruct_split);
+// 4 = one-wave kernel with scalar reads of c_plan instead of LDS tables -- measured
+// slower (8+2 x 64 KiB dual 425 vs 420 us, 12+2 310 vs 305).  Other than 5: sweeps.
+#ifndef DRAID_REC_PLAN
+#define DRAID_REC_PLAN 5
+#endif
 #ifndef DRAID_ENC_SPLIT
 #define DRAID_ENC_SPLIT 0
 #endif
@@ -1581,7 +1777,7 @@ constexpr int rec_waves(int k, int m)
 #define DRAID_REC_SPLIT 0
 #endif
 constexpr int enc_split(int k) { return DRAID_ENC_SPLIT >= 1 ? DRAID_ENC_SPLIT : k <= 2 ? 1 : k <= 7 ? 2 : 4; }
-constexpr int rec_split(int k) { return DRAID_REC_SPLIT >= 1 ? DRAID_REC_SPLIT : k >= 16 ? 4 : 1; }
+constexpr int rec_split(int k) { return DRAID_REC_SPLIT >= 1 ? DRAID_REC_SPLIT : k >= 8 ? 2 : 1; }
 constexpr int enc_split_waves(int k, int m)
 {
     return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES
@@ -1592,7 +1788,11 @@ constexpr int enc_split_waves(int k, int m)
 }
 constexpr int rec_split_waves(int k, int m)
 {
-    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES : rec_split(k) == 1 ? rec_waves(k, m) : 8;
+    return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
+           : rec_split(k) == 1  ? rec_waves(k, m)
+           : DRAID_REC_PLAN != 5 ? 8                      // strips dealt, arithmetic too
+           : (k == 8 && m == 2) ? 6
+                                : 5;
 }
 template <int U, int MAP = 0, int WAVES = 0, int SPLIT = 1>
 using EncCfg = Cfg<kLanes * SPLIT, U, pol_aux(2, 18), MAP, 0, WAVES, SPLIT>;
@@ -1601,12 +1801,6 @@ using EncCfg = Cfg<kLanes * SPLIT, U, pol_aux(2, 18), MAP, 0, WAVES, SPLIT>;
 // lab variant 38 vs 0, median of 5 rounds, profiles/r01/cachepol/xcd_*.json) -- while it
 // costs 2-3% at 4+1 / 8+2 x 64 and 128 KiB, so the smaller k keep stripe order.
 constexpr int enc_map(int k) { return k >= 16 && enc_split(k) == 1 ? 3 : 0; }
-// Plan constants of the one-wave reconstruct: 0 = exp/log tables staged in LDS
-// (production), 4 = scalar reads of c_plan as in the split kernel -- measured
-// slower there (8+2 x 64 KiB dual 425 vs 420 us, 12+2 310 vs 305), sweeps only.
-#ifndef DRAID_REC_PLAN
-#define DRAID_REC_PLAN 0
-#endif
 // Reconstruct load policy: 2 = non-temporal buffer loads as in the encode
 // (production), -1 = non-temporal global loads.  Round 1 measured the global form
 // 1.8% faster at 8+2 x 64 KiB, when the pointer table came through per-lane loads
@@ -1617,7 +1811,8 @@ constexpr int enc_map(int k) { return k >= 16 && enc_split(k) == 1 ? 3 : 0; }
 #define DRAID_REC_LOAD_AUX 2
 #endif
 template <int U, int WAVES = 0, int SPLIT = 1>
-using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(DRAID_REC_LOAD_AUX, 18), 0, DRAID_REC_PLAN, WAVES, SPLIT>;
+using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(DRAID_REC_LOAD_AUX, 18), 0,
+                   (DRAID_REC_PLAN == 5 && SPLIT == 1) ? 0 : DRAID_REC_PLAN, WAVES, SPLIT>;
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 
