@@ -1751,6 +1751,10 @@ constexpr int rec_waves(int k, int m)
 //                12+2 279 vs 297, 14+2 326 vs 358, 16+2 x 256 KiB 380 vs 412;
 //                k = 3..7 two waves (7+2: 361 vs 365, four waves 379; 4+1 194.7 vs 202.6
 //                at 5 per SIMD; 3+1 310.6 vs 318.2; 4+2 239.5 vs 242.3), k = 2 one.
+//                Dealing the encode's arithmetic by column as k_reconstruct_cols does
+//                (no scaling of Q parts, but k KiB through LDS per item and dword
+//                stores) loses or ties at every shape: 8+2 x 64 KiB 399-406 vs 388 us,
+//                4+1 202-211 vs 196, 12+2 282-288 vs 278, 16+2 x 256 KiB 379 vs 379.
 //   reconstruct  dealing the arithmetic by strip as the encode does costs it too much
 //                (failure decode and plan in every wave, the scaling of the Q parts):
 //                with four waves only k = 16 wins (380 vs 399), 14+2 (349 vs 341),
