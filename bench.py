@@ -348,6 +348,8 @@ def main() -> None:
     cfg = CONFIGS[args.config]
     if args.shape:
         sk, sm, skib, sb, sf = args.shape.split(",")
+        if sf not in ("single", "dual") or (sf == "dual" and int(sm) != 2):
+            ap.error("--shape: FAILURES is 'single' or 'dual' (dual needs M = 2)")
         args.config = f"shape_{sk}p{sm}_{skib}k_{sf}"
         cfg = dict(k=int(sk), m=int(sm), strip_kib=int(skib), stripes=int(sb), failures=sf,
                    label=f"lab shape {sk}+{sm} x {skib} KiB, {sf} failure")
