@@ -322,7 +322,7 @@ __device__ __forceinline__ bool stripe_aligned(const Ptrs& pp, uint32_t s, int k
 //   MAP   0: block b -> (stripe b / cps, chunk b % cps)
 //         1: chunk-major (chunk b / nstripes, stripe b % nstripes)
 //         2: persistent grid-stride over stripe-major items
-//   PLAN  (reconstruct) 0: exp/log tables staged in LDS, 1: scalar reads of
+//   PLAN  (one-wave reconstruct) 0: exp/log tables staged in LDS, 1: scalar reads of
 //         the __constant__ tables (no LDS, no barrier)
 //   WAVES waves per SIMD the kernel is built for (0: the compiler's choice).
 //         The compiler pads the register allocation so exactly this many waves
@@ -332,9 +332,9 @@ __device__ __forceinline__ bool stripe_aligned(const Ptrs& pp, uint32_t s, int k
 //         the 7 its 70 VGPRs would allow, 0.417 at 4).
 //   SPLIT waves that share one item: the workgroup has SPLIT * 64 lanes, the item
 //         is still 64 lanes wide (1 KiB of every strip at U = 1), and wave w loads
-//         only strips [w*KW, (w+1)*KW), KW = ceil(k / SPLIT); the partial sums meet
-//         in LDS (k_encode_split / k_reconstruct_split).  NTHR_ counts the lanes of
-//         the whole workgroup.
+//         only strips [w*KW, (w+1)*KW), KW = ceil(k / SPLIT); the encode's partial
+//         sums (k_encode_split) or the reconstruct's raw strips (k_reconstruct_cols)
+//         meet in LDS.  NTHR_ counts the lanes of the whole workgroup.
 template <int NTHR_, int U_, int POL_, int MAP_, int PLAN_ = 0, int WAVES_ = 0, int SPLIT_ = 1>
 struct Cfg {
     static constexpr int NTHR = NTHR_, U = U_, POL = POL_, MAP = MAP_, PLAN = PLAN_,
@@ -902,13 +902,9 @@ __host__ __device__ constexpr uint32_t gf_exp2_const(int e)
     return c;
 }
 
-// Partial sums of one wave (and, in the reconstruct, the plan's tables).
+// Partial sums of one wave.
 struct PartPQ {
     u32x4 p, q;
-};
-struct PartRec {
-    u32x4 p, q;
-    PlanMul mul;
 };
 
 // Returns part(std::integral_constant<int, W>) for the wave's own index W = w
@@ -1042,206 +1038,23 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_split(
     }
 }
 
-// Vector i of every strip.  The surviving P rides on the last wave and the
-// surviving Q on the wave with the fewest data strips left, both folded into the
-// partial syndromes; after the barrier wave 0 writes the first rebuilt strip and
-// the last wave the second, each from the complete syndromes.  The plan's
-// constants come from scalar table reads placed between the issue of the strip
-// loads and their first use.
-template <int KT, int M, int SPLIT, int POL, bool BOUNDED, bool QS, class Ptrs>
-__device__ __forceinline__ void recover_split_vec(const Ptrs& pp, uint32_t s, RecPlan& pl,
-                                                  uint32_t w, uint32_t lane, uint32_t i,
-                                                  uint32_t nvec, SplitLds<SPLIT>& lds)
-{
-    using MW = Mem<u32x4>;
-    static_assert(SPLIT == 2 || SPLIT == 4, "every wave finishes 16 / SPLIT bytes per lane");
-    constexpr int KW = (KT + SPLIT - 1) / SPLIT;
-    constexpr int REM = SPLIT * KW - KT;  // strip slots the last wave leaves empty
-    constexpr uint32_t WP = SPLIT - 1, WQ = REM >= 2 ? SPLIT - 1 : SPLIT - 2;
-    const bool ok = !BOUNDED || i < nvec;
-    const uint8_t* pP = pp.get(s, KT);
-    const uint8_t* pQ = (M == 2) ? pp.get(s, KT + 1) : pP;
-    // fetched before the barrier, while a table read can still be a scalar load
-    const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
-    const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
-    const int x = pl.x, y = pl.y, nd = pl.nd;
-    const uint32_t lost = pl.lost;
-    const bool lostP = pl.lostP, lostQ = pl.lostQ;
-    const bool haveP = !lostP, haveQ = M == 2 && pl.needq && !lostQ;  // wave-uniform
-    const PartRec part = wave_case<0, SPLIT>(w, [=, &pp](auto wc) __attribute__((always_inline)) {
-        constexpr uint32_t W = decltype(wc)::value;
-        constexpr int J0 = static_cast<int>(W) * KW;
-        u32x4 pv = 0, qv = 0, d[KW];
-        if constexpr (W == WP)
-            pv = ok ? MW::template ld_if<POL>(pP, i, haveP) : u32x4(0);
-        if constexpr (W == WQ)
-            qv = ok ? MW::template ld_if<POL>(pQ, i, haveQ) : u32x4(0);
-#pragma unroll
-        for (int j = KW - 1; j >= 0; --j) {
-            const int jj = J0 + j;
-            d[j] = 0;
-            if (jj < KT)  // compile-time once unrolled: a ragged last wave has fewer strips
-                d[j] = ok ? MW::template ld_if<POL>(pp.get(s, jj), i, !((lost >> jj) & 1u))
-                          : u32x4(0);
-        }
-        const PlanMul mul = plan_constants_scalar(nd, x, y, lostP, lostQ);
-        u32x4 ps = 0, qs = 0;
-#pragma unroll
-        for (int j = KW - 1; j >= 0; --j) {
-            ps ^= d[j];
-            if constexpr (M == 2 && QS)
-                qs = gf_mul2(qs) ^ d[j];
-        }
-        if constexpr (M == 2 && QS && J0 != 0)
-            qs = gf_mulc(make_mul_table(gf_exp2_const(J0)), qs);
-        return PartRec{ps ^ pv, qs ^ qv, mul};
-    });
-    pl.t1 = part.mul.t1;
-    pl.t2 = part.mul.t2;
-    lds.p[w][lane] = part.p;
-    if constexpr (M == 2 && QS)
-        lds.q[w][lane] = part.q;
-    __syncthreads();
-    // Every wave finishes a quarter (half, for two waves) of the item: lane l of
-    // wave w owns ND consecutive dwords of the item's 256.  The work after the
-    // barrier -- LDS sums, two constant multiplications, the stores -- is what an
-    // item adds to its memory latency; spread over all waves it is ND/4 of what
-    // two writer waves would each do on whole 16-byte vectors.
-    constexpr int ND = 4 / SPLIT;
-    const uint32_t t = (w * 64u + lane) * ND;
-    const uint32_t ob = ((i - lane) << 4) + t * 4u;  // byte offset in the strip
-    const bool okw = !BOUNDED || ob < (nvec << 4);
-    const uint32_t* lp = reinterpret_cast<const uint32_t*>(lds.p);
-    const uint32_t* lq = reinterpret_cast<const uint32_t*>(lds.q);
-    uint32_t pt[ND], qt[ND];
-#pragma unroll
-    for (int n = 0; n < ND; ++n) {
-        pt[n] = lp[t + n];
-        qt[n] = 0;
-#pragma unroll
-        for (int u = 1; u < SPLIT; ++u)
-            pt[n] ^= lp[u * 256 + t + n];
-        if constexpr (M == 2 && QS) {
-            qt[n] = lq[t + n];
-#pragma unroll
-            for (int u = 1; u < SPLIT; ++u)
-                qt[n] ^= lq[u * 256 + t + n];
-        }
-    }
-    if (!okw)
-        return;
-    uint32_t o1[ND], o2[ND];
-    if (pl.nd == 0) {
-        if (pl.lostP)
-            st_words<POL, ND>(pP, ob, pt);
-        if (M == 2 && pl.lostQ)
-            st_words<POL, ND>(pQ, ob, qt);
-    } else if (pl.nd == 1) {
-        if (!pl.lostP) {
-            st_words<POL, ND>(pX, ob, pt);
-            if (M == 2 && pl.lostQ) {
-#pragma unroll
-                for (int n = 0; n < ND; ++n)
-                    o2[n] = qt[n] ^ gf_mulc(pl.t1, pt[n]);
-                st_words<POL, ND>(pQ, ob, o2);
-            }
-        } else {
-#pragma unroll
-            for (int n = 0; n < ND; ++n) {
-                o1[n] = gf_mulc(pl.t1, qt[n]);
-                o2[n] = pt[n] ^ o1[n];
-            }
-            st_words<POL, ND>(pX, ob, o1);
-            st_words<POL, ND>(pP, ob, o2);
-        }
-    } else {
-#pragma unroll
-        for (int n = 0; n < ND; ++n) {
-            o1[n] = gf_mulc(pl.t1, pt[n]) ^ gf_mulc(pl.t2, qt[n]);
-            o2[n] = pt[n] ^ o1[n];
-        }
-        st_words<POL, ND>(pX, ob, o1);
-        st_words<POL, ND>(pY, ob, o2);
-    }
-}
-
-template <int KT, int M, class C, class Ptrs>
-__device__ __forceinline__ void reconstruct_item_split(const Ptrs& pp, uint32_t s, uint32_t c,
-                                                       uint32_t len, uint32_t cps, RecPlan& pl,
-                                                       bool aligned, SplitLds<C::SPLIT>& lds)
-{
-    constexpr int SPLIT = C::SPLIT, POL = C::POL;
-    constexpr uint32_t L = 64;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t nvec = len >> 4;
-    auto none = [](RecPlan&) {};
-    if (aligned) {
-        const uint32_t i = c * L + lane;
-        if ((c + 1) * L <= nvec) {
-            if (M == 2 && !pl.needq)  // wave-uniform
-                recover_split_vec<KT, M, SPLIT, POL, false, false>(pp, s, pl, w, lane, i, nvec,
-                                                                   lds);
-            else
-                recover_split_vec<KT, M, SPLIT, POL, false, true>(pp, s, pl, w, lane, i, nvec,
-                                                                  lds);
-        } else {
-            recover_split_vec<KT, M, SPLIT, POL, true, true>(pp, s, pl, w, lane, i, nvec, lds);
-        }
-        // recover_split_vec left the plan's constants in pl
-        const uint32_t tail = len & 15u;
-        if (w == 0 && tail && c == cps - 1 && lane < tail)
-            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, nvec * 16 + lane,
-                                                                   L, len, none);
-    } else if (w == 0) {
-        const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
-        pl.t1 = mul.t1;
-        pl.t2 = mul.t2;
-        const uint32_t b1 = min(len, (c + 1) * L * 16);
-        for (uint32_t b = c * L * 16 + lane; b < b1; b += L)
-            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, b, L, b1, none);
-    }
-}
-
-template <int KT, int M, class C, class Ptrs>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_split(
-    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, const uint8_t* fail, uint32_t f01,
-    uint32_t* bad)
-{
-    static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one split item per workgroup, stripe order");
-    __shared__ SplitLds<C::SPLIT> lds;
-    const uint32_t c = blockIdx.x, s = blockIdx.z * kGridY + blockIdx.y;
-    if (s >= nstripes)
-        return;  // uniform: the ragged last z-slice
-    // The pointer row and the failure pair are independent scalar reads: both are
-    // issued before either is used, so an item pays one memory round trip for
-    // them, not two, before its strip loads can go out.
-    const bool aligned = stripe_aligned<KT, M>(pp, s, KT);
-    uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
-    if (fail) {
-        const uint32_t f = load_fail_pair(fail, s);
-        f0 = f & 0xffu;
-        f1 = f >> 8;
-    }
-    RecPlan pl = decode_failures_mask<KT, M>(f0, f1);
-    const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
-    if (!pl.skip)  // uniform across the workgroup
-        reconstruct_item_split<KT, M, C>(pp, s, c, len, cps, pl, aligned, lds);
-    if (count_bad)  // after the item: nothing may be stored ahead of its pointer reads
-        atomicAdd(bad, 1u);
-}
-
-// ---- loads dealt by strip, arithmetic dealt by column
+// ---- shared reconstruct: loads dealt by strip, arithmetic dealt by column
 //
-// The shared reconstruct above splits the ARITHMETIC by strip as well: every wave
-// runs a Horner chain over its strips on whole 16-byte vectors and its Q part then
-// needs a constant multiplication to line up (36 VALU per wave), which is what a
-// VALU-heavy dual-failure rebuild cannot afford (8+2: 580 VALU per item against
-// 435 for one wave).  Here only the LOADS are dealt by strip: each wave loads its
-// strips as 16-byte vectors and parks them in LDS untouched (one row per strip;
-// a strip that is lost or not needed arrives as zeros through a descriptor with no
-// records).  After one barrier every wave owns a quarter of the item's 256 dword
-// columns and runs the one Horner chain down all k strips of its columns: the
-// same arithmetic as the one-wave kernel, no scaling, spread evenly over the waves.
+// Dealing the reconstruct's ARITHMETIC by strip as the encode does (a Horner chain
+// per wave over its strips on whole 16-byte vectors, the Q part scaled by a
+// constant to line up, parts XORed through LDS) was built and measured: the
+// scaling costs 36 VALU per wave, which a VALU-heavy dual-failure rebuild cannot
+// afford (8+2: 580 VALU per item against 435 for one wave), and it lost to the
+// one-wave kernel below k = 16 (profiles/r02/split/).  Here only the LOADS are
+// dealt by strip: each wave loads its strips as 16-byte vectors and parks them in
+// LDS untouched (one row per strip; a strip that is lost or not needed arrives as
+// zeros through a descriptor with no records).  The surviving P rides on the last
+// wave and the surviving Q on the wave with the fewest data strips.  The plan's
+// constants come from scalar table reads placed between the issue of the strip
+// loads and the barrier.  After the one barrier every wave owns its share of the
+// item's 256 dword columns and runs the one Horner chain down all k strips of its
+// columns: the same arithmetic as the one-wave kernel, no scaling, spread evenly
+// over the waves whatever the failure pattern.
 template <int KT>
 struct ColLds {
     u32x4 row[KT + 2][64];  // rows 0..KT-1 data strips, KT the surviving P, KT+1 the surviving Q
@@ -1674,12 +1487,8 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
         return hipSuccess;
     if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    if constexpr (C::SPLIT > 1 && C::PLAN == 5)
+    if constexpr (C::SPLIT > 1)
         hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), split_grid(cps, nstripes),
-                           dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
-                           fail, f01, bad);
-    else if constexpr (C::SPLIT > 1)
-        hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), split_grid(cps, nstripes),
                            dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
                            fail, f01, bad);
     else
@@ -1757,8 +1566,9 @@ constexpr int rec_waves(int k, int m)
 //                4+1 202-211 vs 196, 12+2 282-288 vs 278, 16+2 x 256 KiB 379 vs 379.
 //   reconstruct  dealing the arithmetic by strip as the encode does costs it too much
 //                (failure decode and plan in every wave, the scaling of the Q parts):
-//                with four waves only k = 16 wins (380 vs 399), 14+2 (349 vs 341),
-//                12+2 (330 vs 305) and 8+2 dual (447 vs 420) lose.  Dealing only the
+//                with four waves only k = 16 won (380 vs 399), 14+2 (349 vs 341),
+//                12+2 (330 vs 305) and 8+2 dual (447 vs 420) lost; that kernel is no
+//                longer in the source.  Dealing only the
 //                LOADS by strip and the arithmetic by column (k_reconstruct_cols), two
 //                waves per item, wins from k = 8 up against the one-wave kernel at its
 //                best occupancy: 8+1 365.6 vs 376.7, 10+2 480 vs 494, 12+2 288 vs 298.7,
@@ -1766,13 +1576,12 @@ constexpr int rec_waves(int k, int m)
 //                381 (= four waves by strip); four waves lose below k = 16 (8+2 dual 478),
 //                k <= 7 stays one wave (6+2: 323 vs 322).
 // DRAID_ENC_SPLIT / DRAID_REC_SPLIT (>= 1) override every k, for sweeps only.
-// How a shared reconstruct item is divided (the one-wave kernel always stages the
-// exp/log tables in LDS): 5 = loads by strip, arithmetic by column (production,
-// k_reconstruct_cols), 0 = loads and arithmetic by strip (k_reconstruct_split);
-// 4 = one-wave kernel with scalar reads of c_plan instead of LDS tables -- measured
-// slower (8+2 x 64 KiB dual 425 vs 420 us, 12+2 310 vs 305).  Other than 5: sweeps.
+// Where the one-wave reconstruct takes its plan constants from: 0 = exp/log tables
+// staged in LDS (production), 4 = scalar reads of c_plan, no LDS -- measured slower
+// (8+2 x 64 KiB dual 425 vs 420 us, 12+2 310 vs 305), sweeps only.  The shared
+// reconstruct always reads c_plan.
 #ifndef DRAID_REC_PLAN
-#define DRAID_REC_PLAN 5
+#define DRAID_REC_PLAN 0
 #endif
 #ifndef DRAID_ENC_SPLIT
 #define DRAID_ENC_SPLIT 0
@@ -1794,7 +1603,6 @@ constexpr int rec_split_waves(int k, int m)
 {
     return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
            : rec_split(k) == 1  ? rec_waves(k, m)
-           : DRAID_REC_PLAN != 5 ? 8                      // strips dealt, arithmetic too
            : (k == 8 && m == 2) ? 6
                                 : 5;
 }
@@ -1815,8 +1623,7 @@ constexpr int enc_map(int k) { return k >= 16 && enc_split(k) == 1 ? 3 : 0; }
 #define DRAID_REC_LOAD_AUX 2
 #endif
 template <int U, int WAVES = 0, int SPLIT = 1>
-using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(DRAID_REC_LOAD_AUX, 18), 0,
-                   (DRAID_REC_PLAN == 5 && SPLIT == 1) ? 0 : DRAID_REC_PLAN, WAVES, SPLIT>;
+using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(DRAID_REC_LOAD_AUX, 18), 0, DRAID_REC_PLAN, WAVES, SPLIT>;
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 

@@ -165,7 +165,8 @@ def test_gf_vect_mul_every_constant(ec):
     assert (host(d2[5:5 + L]) == ref).all()
 
 
-@pytest.mark.parametrize("k,m", [(2, 1), (4, 1), (8, 2), (9, 2), (14, 2), (16, 2), (40, 2)])
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 1), (8, 1), (16, 1), (8, 2), (9, 2), (10, 2), (12, 2), (14, 2),
+                                 (16, 2), (40, 2)])
 def test_recover_every_failure_set(ec, k, m):
     L = 4096
     rng = np.random.default_rng(k)
