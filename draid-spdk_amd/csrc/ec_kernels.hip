@@ -1317,68 +1317,100 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_w
 // raid5.c:705-741, extended to Q): for the nd data chunks a segment touches,
 // with old contents O_i and new contents N_i at data index e_i,
 //   P' = P ^ XOR_i (O_i ^ N_i),   Q' = Q ^ XOR_i 2^{e_i} (O_i ^ N_i).
-// The Q sum is a Horner evaluation with gaps over the exponents, sorted
-// descending by the host: q = mul2^(e_prev - e_i)(q) ^ delta_i, then
-// mul2^(e_last)(q) -- at most k-1 doublings per element, no table lookups.
-// Segment table row: [O_0, N_0, O_1, N_1, ..., P, (Q)]; exps row: e_0 > e_1 > ...
-template <int M, class C>
-__global__ __launch_bounds__(C::NTHR) void k_update_work(const uint8_t* const* tab, uint32_t nd,
-                                                         const uint8_t* exps, WorkSrc ws,
-                                                         uint32_t nwork)
+// Each 2^{e_i} is a constant multiplication through the ready-made table of that
+// power (c_plan.mul, a scalar read): 9 VALU operations per dword whatever the
+// exponent, against up to k-1 doublings of 6.
+// Segment table row: [O_0, N_0, O_1, N_1, ..., P, (Q)]; exps row: e_0, e_1, ...
+// The row and the exponents are read through the constant address space, so the
+// strip bases stay in SGPRs (a base in VGPRs costs a readfirstlane loop around
+// every buffer access).  NDT = 1, 2: nd at compile time, every load of the item
+// issued before the first use; NDT = 0: run-time nd.
+
+// Byte idx of a device byte array that the kernel never writes: a scalar load of
+// the aligned word around it.
+__device__ __forceinline__ uint32_t load_const_byte(const uint8_t* a, size_t idx)
+{
+    const uintptr_t p = reinterpret_cast<uintptr_t>(a) + idx;
+    typedef const uint32_t __attribute__((address_space(4)))* ccw;
+    const uint32_t w = ((ccw)(p & ~static_cast<uintptr_t>(3)))[0];
+    return (w >> ((static_cast<uint32_t>(p) & 3u) * 8u)) & 0xffu;
+}
+
+template <int M, int NDT, class C>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_update_work(
+    const uint8_t* const* tab, uint32_t nd_rt, const uint8_t* exps, WorkSrc ws, uint32_t nwork)
 {
     constexpr uint32_t EPB = static_cast<uint32_t>(C::NTHR) * C::U;
-    const uint32_t stride = 2 * nd + M;
-    for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
-        WorkItem w;
-        uint32_t len, cps_w;
-        ws.get(b, EPB * 16, w.seg, w.chunk, len, cps_w);
-        const uint8_t* const* row = tab + (size_t)w.seg * stride;
-        const uint8_t* ex = exps + (size_t)w.seg * nd;
-        const uint8_t* pP = row[2 * nd];
-        const uint8_t* pQ = M == 2 ? row[2 * nd + 1] : pP;
-        uintptr_t acc = 0;
-        for (uint32_t t = 0; t < stride; ++t)
-            acc |= reinterpret_cast<uintptr_t>(row[t]);
-        auto body = [&](auto tag, uint32_t i) {
-            using W = decltype(tag);
-            using MW = Mem<W>;
-            W dp = W(0), dq = W(0);
-            int prev = -1;
-            for (uint32_t t = 0; t < nd; ++t) {
-                const W delta = MW::template ld<C::POL>(row[2 * t], i) ^
-                                MW::template ld<C::POL>(row[2 * t + 1], i);
+    static_assert(C::U == 1, "one vector per lane");
+    const uint32_t nd = NDT > 0 ? NDT : nd_rt;
+    const uint32_t b = blockIdx.x;  // one work item per workgroup
+    if (b >= nwork)
+        return;
+    uint32_t seg, chunk, len, cps;
+    ws.get(b, EPB * 16, seg, chunk, len, cps);
+    const TablePtrs row{tab, 2 * nd + M};
+    const uint8_t* pP = row.get(seg, static_cast<int>(2 * nd));
+    const uint8_t* pQ = M == 2 ? row.get(seg, static_cast<int>(2 * nd + 1)) : pP;
+    uintptr_t acc = reinterpret_cast<uintptr_t>(pP) | reinterpret_cast<uintptr_t>(pQ);
+    if constexpr (NDT > 0) {
+#pragma unroll
+        for (int t = 0; t < 2 * NDT; ++t)
+            acc |= reinterpret_cast<uintptr_t>(row.get(seg, t));
+    } else {
+        for (uint32_t t = 0; t < 2 * nd; ++t)
+            acc |= reinterpret_cast<uintptr_t>(row.get(seg, static_cast<int>(t)));
+    }
+    const size_t e0 = static_cast<size_t>(seg) * nd;
+    auto body = [&](auto tag, uint32_t i) __attribute__((always_inline)) {
+        using W = decltype(tag);
+        using MW = Mem<W>;
+        W dp = W(0), dq = W(0);
+        if constexpr (NDT > 0) {
+            W o[NDT], n[NDT];
+#pragma unroll
+            for (int t = 0; t < NDT; ++t) {
+                o[t] = MW::template ld<C::POL>(row.get(seg, 2 * t), i);
+                n[t] = MW::template ld<C::POL>(row.get(seg, 2 * t + 1), i);
+            }
+            const W p0 = MW::template ld<C::POL>(pP, i);
+            const W q0 = M == 2 ? MW::template ld<C::POL>(pQ, i) : W(0);
+#pragma unroll
+            for (int t = 0; t < NDT; ++t) {
+                const W delta = o[t] ^ n[t];
                 dp ^= delta;
-                if constexpr (M == 2) {
-                    const int e = ex[t];
-                    for (int g = (prev < 0 ? 0 : prev - e); g > 0; --g)
-                        dq = gf_mul2(dq);
-                    dq ^= delta;
-                    prev = e;
-                }
+                if constexpr (M == 2)
+                    dq ^= gf_mulc(mul_table_exp2(load_const_byte(exps, e0 + t)), delta);
             }
-            MW::template st<C::POL>(pP, i, MW::template ld<C::POL>(pP, i) ^ dp);
-            if constexpr (M == 2) {
-                for (int g = prev; g > 0; --g)
-                    dq = gf_mul2(dq);
-                MW::template st<C::POL>(pQ, i, MW::template ld<C::POL>(pQ, i) ^ dq);
-            }
-        };
-        if ((acc & 15u) == 0) {
-            const uint32_t nvec = len >> 4;
-            for (uint32_t u = 0; u < C::U; ++u) {
-                const uint32_t i = w.chunk * EPB + u * C::NTHR + threadIdx.x;
-                if (i < nvec)
-                    body(u32x4{}, i);
-            }
-            const uint32_t tail = len & 15u;
-            const uint32_t cps = cps_w;
-            if (tail && w.chunk == cps - 1 && threadIdx.x < tail)
-                body(uint32_t{}, nvec * 16 + threadIdx.x);
+            MW::template st<C::POL>(pP, i, p0 ^ dp);
+            if constexpr (M == 2)
+                MW::template st<C::POL>(pQ, i, q0 ^ dq);
         } else {
-            const uint32_t b1 = min(len, (w.chunk + 1) * EPB * 16);
-            for (uint32_t i = w.chunk * EPB * 16 + threadIdx.x; i < b1; i += C::NTHR)
-                body(uint32_t{}, i);
+            const W p0 = MW::template ld<C::POL>(pP, i);
+            const W q0 = M == 2 ? MW::template ld<C::POL>(pQ, i) : W(0);
+            for (uint32_t t = 0; t < nd; ++t) {
+                const W delta = MW::template ld<C::POL>(row.get(seg, static_cast<int>(2 * t)), i) ^
+                                MW::template ld<C::POL>(row.get(seg, static_cast<int>(2 * t + 1)), i);
+                dp ^= delta;
+                if constexpr (M == 2)
+                    dq ^= gf_mulc(mul_table_exp2(load_const_byte(exps, e0 + t)), delta);
+            }
+            MW::template st<C::POL>(pP, i, p0 ^ dp);
+            if constexpr (M == 2)
+                MW::template st<C::POL>(pQ, i, q0 ^ dq);
         }
+    };
+    if ((acc & 15u) == 0) {
+        const uint32_t nvec = len >> 4;
+        const uint32_t i = chunk * EPB + threadIdx.x;
+        if (i < nvec)
+            body(u32x4{}, i);
+        const uint32_t tail = len & 15u;
+        if (tail && chunk == cps - 1 && threadIdx.x < tail)
+            body(uint32_t{}, nvec * 16 + threadIdx.x);
+    } else {
+        const uint32_t b1 = min(len, (chunk + 1) * EPB * 16);
+        for (uint32_t i = chunk * EPB * 16 + threadIdx.x; i < b1; i += C::NTHR)
+            body(uint32_t{}, i);
     }
 }
 
@@ -1946,21 +1978,39 @@ hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const*
     }
 }
 
+// Waves per SIMD of the update kernel: 4 measured best on the scatter-gather
+// benchmark's window (one 64 KiB chunk per 8+2 stripe, ms per 4096 stripes: 0.268
+// vs 0.272 at the compiler's choice, 0.270 at 6, 0.274 at 8; 4 KiB runs 0.307 vs
+// 0.311; profiles/r02/sg/update_kernel_ab.jsonl).
+#ifndef DRAID_UPD_WAVES
+#define DRAID_UPD_WAVES 4
+#endif
+template <int M, int NDT>
+static hipError_t go_update_work(uint32_t nd, const uint8_t* const* table, const uint8_t* exps,
+                                 const uint32_t* seg_len, const void* work, uint32_t ulen,
+                                 uint32_t nwork, hipStream_t st)
+{
+    using C = EncCfg<1, 0, DRAID_UPD_WAVES>;  // buffer nt loads, write-through nt stores
+    const WorkSrc ws = work_src<C>(seg_len, work, ulen);
+    hipLaunchKernelGGL((k_update_work<M, NDT, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
+                       exps, ws, nwork);
+    return hipGetLastError();
+}
+
 hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* table,
                               const uint8_t* exps, const uint32_t* seg_len, const void* work,
                               uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
-    using C = EncCfg<1>;  // buffer nt loads, write-through nt stores
     if (nwork == 0)
         return hipSuccess;
-    const WorkSrc ws = work_src<C>(seg_len, work, ulen);
+    if (nd == 0 || (m != 1 && m != 2))
+        return hipErrorInvalidValue;
+#define DRAID_UPD(M_, ND_) \
+    go_update_work<M_, ND_>(nd, table, exps, seg_len, work, ulen, nwork, st)
     if (m == 1)
-        hipLaunchKernelGGL((k_update_work<1, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
-                           exps, ws, nwork);
-    else
-        hipLaunchKernelGGL((k_update_work<2, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
-                           exps, ws, nwork);
-    return hipGetLastError();
+        return nd == 1 ? DRAID_UPD(1, 1) : nd == 2 ? DRAID_UPD(1, 2) : DRAID_UPD(1, 0);
+    return nd == 1 ? DRAID_UPD(2, 1) : nd == 2 ? DRAID_UPD(2, 2) : DRAID_UPD(2, 0);
+#undef DRAID_UPD
 }
 
 hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,

@@ -61,6 +61,49 @@ def test_rmw_update_matches_reencode(ec, k, m, L, B):
     assert (got[:, :k] == host[:, :k]).all()      # update touches parity only
 
 
+@pytest.mark.parametrize("nd", [1, 2, 3])
+@pytest.mark.parametrize("k,m", [(4, 1), (8, 2), (16, 2), (40, 2)])
+def test_rmw_each_touched_count_and_exponent(ec, k, m, nd):
+    """nd = 1 and 2 have kernels of their own, 3 runs the run-time loop; over the
+    batch every data index (every power of two up to 2^(k-1)) multiplies a delta,
+    in both orders, on whole strips (16-byte vectors plus a ragged tail)."""
+    L = 4096 + 16 + 5
+    B = 2 * k
+    n = k + m
+    rng = np.random.default_rng(7000 + 10 * k + nd)
+    host = np.zeros((B, n, L), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    assert oracle.encode_strided(host.reshape(-1), k, m, L, B, L, n * L) == 0
+    stripes = torch.from_numpy(host.copy()).to(DEV)
+    newdata = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).to(DEV)
+    olddata = stripes[:, :k].clone()
+    torch.cuda.synchronize()
+    expect = host.copy()
+    ctx = ec.Ctx()
+    try:
+        for s in range(B):
+            idx = [(s + 5 * t) % k for t in range(nd)]
+            if len(set(idx)) != nd:
+                idx = [(s + t) % k for t in range(nd)]
+            if s >= k:
+                idx = idx[::-1]
+            old = [[(olddata[s, i].data_ptr(), L)] for i in idx]
+            new = [[(newdata[s, i].data_ptr(), L)] for i in idx]
+            par = [[(stripes[s, k + j].data_ptr(), L)] for j in range(m)]
+            assert ctx.update_sg(k, m, idx, old, new, par, L) == 0
+            for i in idx:
+                expect[s, i] = newdata[s, i].cpu().numpy()
+        ctx.flush()
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    ref = expect.copy()
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, B, L, n * L) == 0
+    got = stripes.cpu().numpy()
+    assert (got[:, k:] == ref[:, k:]).all()
+    assert (got[:, :k] == host[:, :k]).all()
+
+
 def test_rmw_rejects_bad_indices(ec):
     ctx = ec.Ctx()
     try:
