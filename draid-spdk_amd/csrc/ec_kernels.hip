@@ -251,6 +251,37 @@ __device__ __forceinline__ void for_sources_desc(int k, F&& f)
     }
 }
 
+// Run-time stripe width (k without an unrolled instance): the strips in blocks of
+// kRtBlock, from the top down, every load of a block issued before the block's
+// arithmetic -- a plain loop over j would wait for each strip before asking for
+// the next.  The top block may reach past strip k-1: those slots load nothing
+// (ld_if with live == false, through the pointer of strip k-1, never one past the
+// row) and hand zeros to acc, which a Horner chain that is still zero ignores.
+// live(j): wave-uniform, false for a strip that must not be read.
+constexpr int kRtBlock = 8;
+template <int U, int POL, class W, class Ptrs, class Live, class Acc>
+__device__ __forceinline__ void for_blocks_desc(const Ptrs& pp, uint32_t s, int k,
+                                                const bool (&ok)[U], uint32_t i0,
+                                                uint32_t stride, Live&& live, Acc&& acc)
+{
+    using MW = Mem<W>;
+    for (int jb = ((k + kRtBlock - 1) / kRtBlock) * kRtBlock; jb > 0; jb -= kRtBlock) {
+        W d[kRtBlock][U];
+#pragma unroll
+        for (int t = kRtBlock - 1; t >= 0; --t) {
+            const int j = jb - kRtBlock + t;
+            const bool on = j < k && live(j);
+            const uint8_t* src = pp.get(s, j < k ? j : k - 1);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                d[t][u] = ok[u] ? MW::template ld_if<POL>(src, i0 + u * stride, on) : W(0);
+        }
+#pragma unroll
+        for (int t = kRtBlock - 1; t >= 0; --t)
+            acc(d[t]);
+    }
+}
+
 // ------------------------------------------------------------ encode core
 
 // Computes P (and Q for M == 2) over the U elements i0 + u*stride (< n) and
@@ -270,16 +301,29 @@ __device__ __forceinline__ bool encode_elems(const Ptrs& pp, uint32_t s, int k, 
         p[u] = W(0);
         q[u] = W(0);
     }
-    for_sources_desc<KT>(k, [&](int j) {
-        const uint8_t* src = pp.get(s, j);
+    if constexpr (KT > 0) {
+        for_sources_desc<KT>(k, [&](int j) {
+            const uint8_t* src = pp.get(s, j);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const W d = ok[u] ? MW::template ld<POL>(src, i0 + u * stride) : W(0);
-            p[u] ^= d;
-            if constexpr (M == 2)
-                q[u] = gf_mul2(q[u]) ^ d;
-        }
-    });
+            for (int u = 0; u < U; ++u) {
+                const W d = ok[u] ? MW::template ld<POL>(src, i0 + u * stride) : W(0);
+                p[u] ^= d;
+                if constexpr (M == 2)
+                    q[u] = gf_mul2(q[u]) ^ d;
+            }
+        });
+    } else {
+        for_blocks_desc<U, POL, W>(
+            pp, s, k, ok, i0, stride, [](int) { return true; },
+            [&](const W(&d)[U]) __attribute__((always_inline)) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    p[u] ^= d[u];
+                    if constexpr (M == 2)
+                        q[u] = gf_mul2(q[u]) ^ d[u];
+                }
+            });
+    }
     const uint8_t* dp = pp.get(s, k);
     const uint8_t* dq = (M == 2) ? pp.get(s, k + 1) : nullptr;
     bool bad = false;
@@ -571,20 +615,29 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
         pv[u] = (useP && ok[u]) ? MW::template ld<POL>(pP, i0 + u * stride) : W(0);
         qv[u] = (useQ && ok[u]) ? MW::template ld<POL>(pQ, i0 + u * stride) : W(0);
     }
-    for_sources_desc<KT>(k, [&](int j) {
-        const bool live = (j != pl.x) && (j != pl.y);
-        W d[U];
-        const uint8_t* src = pp.get(s, j);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            d[u] = (live && ok[u]) ? MW::template ld<POL>(src, i0 + u * stride) : W(0);
+    auto fold = [&](const W(&d)[U]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             ps[u] ^= d[u];
             if constexpr (M == 2 && QS)
                 qs[u] = gf_mul2(qs[u]) ^ d[u];
         }
-    });
+    };
+    if constexpr (KT > 0) {
+        for_sources_desc<KT>(k, [&](int j) {
+            const bool live = (j != pl.x) && (j != pl.y);
+            W d[U];
+            const uint8_t* src = pp.get(s, j);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                d[u] = (live && ok[u]) ? MW::template ld<POL>(src, i0 + u * stride) : W(0);
+            fold(d);
+        });
+    } else {
+        const int x = pl.x, y = pl.y;
+        for_blocks_desc<U, POL, W>(
+            pp, s, k, ok, i0, stride, [=](int j) { return j != x && j != y; }, fold);
+    }
     constants(pl);
     const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
     const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
@@ -1259,9 +1312,16 @@ struct WorkSrc {
     }
 };
 
+// Pointer-table reads of the one-wave work-list encode: ordinary reads for a
+// compiled width (the compiler makes them scalar loads, measured 2% faster than
+// constant-space reads there), constant-space reads for a run-time width, whose
+// strip index is a loop variable.
+template <int KT>
+using WorkEncPtrs = std::conditional_t<(KT > 0), TablePlain, TablePtrs>;
+
 template <int KT, int M, bool CHECK, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(TablePlain pp, uint32_t k_rt, WorkSrc ws,
-                                                         uint32_t nwork)
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(
+    WorkEncPtrs<KT> pp, uint32_t k_rt, WorkSrc ws, uint32_t nwork)
 {
     constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
     const int k = KT > 0 ? KT : static_cast<int>(k_rt);
@@ -1500,7 +1560,7 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
         hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), split_grid(cps, nstripes),
                            dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
                            flag);
-    else if constexpr (std::is_same<Ptrs, TablePtrs>::value)
+    else if constexpr (KT > 0 && std::is_same<Ptrs, TablePtrs>::value)
         hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), 0,
                            st, TablePlain{pp.tab, pp.stride}, k, static_cast<uint32_t>(len), cps,
                            nstripes, flag);
@@ -1659,8 +1719,21 @@ using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(DRAID_REC_LOAD_AUX, 18), 0, DRAID_
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 
+// Waves per SIMD of the run-time-width kernels (k > 16; kRtBlock loads per wave and
+// block), same-box A/B of whole library builds, microseconds per launch
+// (profiles/r02/occupancy/runtime_width_waves.jsonl): encode 18+2 x 64 KiB x 2048
+// stripes 409 at 3, 414 at 4, 423 at 5, 431 at 6, 444 at 2; 32+2 x 1024 stripes 353 /
+// 358 / 369 / 373; reconstruct (dual) 18+2 438 at 3, 446 at 4, 458 at 5, 498 at 2;
+// 32+2 380 / 388 / 397.
+#ifndef DRAID_RT_ENC_WAVES
+#define DRAID_RT_ENC_WAVES 3
+#endif
+#ifndef DRAID_RT_REC_WAVES
+#define DRAID_RT_REC_WAVES 3
+#endif
 // k values with a fully unrolled instantiation; others use the runtime-k loop.
-#define DRAID_FOR_EACH_K(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(12) X(14) X(16)
+#define DRAID_FOR_EACH_K(X) \
+    X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 
 template <int M, class Ptrs>
 static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
@@ -1675,7 +1748,8 @@ static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return go_encode<0, M, false, EncCfg<2>>(pp, k, len, nstripes, nullptr, st);
+        return go_encode<0, M, false, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(pp, k, len, nstripes,
+                                                                         nullptr, st);
     }
 }
 
@@ -1693,7 +1767,8 @@ static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return go_reconstruct<0, M, RecCfg<2>>(pp, k, len, nstripes, fail, f01, bad, st);
+        return go_reconstruct<0, M, RecCfg<1, DRAID_RT_REC_WAVES>>(pp, k, len, nstripes, fail,
+                                                                   f01, bad, st);
     }
 }
 
@@ -1898,7 +1973,8 @@ static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, const ui
                            TablePtrs{tab, k + M}, work_src<C>(seg_len, work, ulen), nwork);
     else
         hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                           TablePlain{tab, k + M}, k, work_src<C>(seg_len, work, ulen), nwork);
+                           WorkEncPtrs<KT>{tab, k + M}, k, work_src<C>(seg_len, work, ulen),
+                           nwork);
     return hipGetLastError();
 }
 
@@ -1919,8 +1995,8 @@ static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t tstrid
 uint32_t work_chunk_bytes(int op, uint32_t k)
 {
     if (op == 2)
-        return kLanes * 1u * 16u;  // update: CfgDefault<1>
-    int u = 2;
+        return kLanes * 1u * 16u;  // update: one vector per lane
+    int u = 1;  // run-time widths
     switch (k) {
 #define DRAID_CASE(K)                                       \
     case K:                                                 \
@@ -1951,8 +2027,10 @@ hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* tabl
 #undef DRAID_CASE
     default:
         return m == 1
-                   ? go_encode_work<0, 1, EncCfg<2>>(table, k, seg_len, work, ulen, nwork, st)
-                   : go_encode_work<0, 2, EncCfg<2>>(table, k, seg_len, work, ulen, nwork, st);
+                   ? go_encode_work<0, 1, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(table, k, seg_len, work,
+                                                                            ulen, nwork, st)
+                   : go_encode_work<0, 2, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(table, k, seg_len, work,
+                                                                            ulen, nwork, st);
     }
 }
 
@@ -1971,10 +2049,10 @@ hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const*
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
-        return m == 1 ? go_reconstruct_work<0, 1, RecCfg<2>>(table, tstride, k, seg_len, fail,
-                                                                 fstride, work, ulen, nwork, st)
-                      : go_reconstruct_work<0, 2, RecCfg<2>>(table, tstride, k, seg_len, fail,
-                                                                 fstride, work, ulen, nwork, st);
+        return m == 1 ? go_reconstruct_work<0, 1, RecCfg<1, DRAID_RT_REC_WAVES>>(
+                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st)
+                      : go_reconstruct_work<0, 2, RecCfg<1, DRAID_RT_REC_WAVES>>(
+                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
     }
 }
 

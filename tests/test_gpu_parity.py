@@ -498,7 +498,7 @@ def test_full_size_linearity(ec, k, m, L, B):
 
 # ------------------------------------------------------------ items shared by several waves
 
-SPLIT_K = [5, 6, 7, 8, 10, 12, 14, 16]   # stripe widths whose items are dealt over 2 or 4 waves
+SPLIT_K = [5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16]   # stripe widths whose items are dealt over 2 or 4 waves
 
 
 @pytest.mark.parametrize("m", [1, 2])
