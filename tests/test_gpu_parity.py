@@ -256,7 +256,10 @@ CONFIGS = [  # (k, m, strip bytes, stripes) -- BASELINE.json configs at reduced 
     (8, 2, 131072, 32),
     (16, 2, 262144, 16),
     (14, 2, 4096, 33),
-    (11, 2, 4096 + 48, 7),   # runtime-k kernel, ragged length
+    (11, 2, 4096 + 48, 7),   # odd width, ragged length
+    (17, 2, 4096 + 48, 7),   # run-time width: one full block of 8 strips and a ragged top block
+    (24, 1, 2048, 9),        # run-time width, whole blocks only
+    (33, 2, 1024 + 7, 5),    # run-time width, five blocks, byte tail
     (6, 1, 1000, 5),         # ragged length, odd size
 ]
 
