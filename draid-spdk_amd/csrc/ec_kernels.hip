@@ -1476,19 +1476,50 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_update_work(
 
 // ------------------------------------------------------------ gf_vect_mul
 
-__global__ __launch_bounds__(kThreads) void k_gf_vect_mul(const uint8_t* src, uint8_t* dst,
-                                                          uint32_t len, NibTable t)
+// dst = c * src through the caller's table (gf_vect_mul.c:108 call shape).  T is the
+// table form: the caller's two 16-entry nibble tables as they are (NibTable, 22
+// VALU operations per dword), or -- when the host found the table to be a linear
+// map, as every table from gf_vect_mul_init is -- the same map as three 3-bit
+// tables (MulTable, 9 operations).  One workgroup per NTHR * U vectors, no
+// grid-stride loop; POL as in the encode.  Measured through the synchronous call
+// on 1 GiB / 256 MiB (GB/s of read + write, tools/gpu_gfv_ab.sh, profiles/r02/
+// gf_vect_mul_ab.jsonl): one wave x one vector 6.51 / 5.89, 256 lanes x 1 6.41 /
+// 5.73, 256 x 2 5.97 / 5.51, 256 x 4 5.82 / 5.25, 64 x 4 6.14 / 5.47; global nt
+// instead of buffer accesses 6.32, plain 6.04.  The grid-stride kernel with the
+// nibble tables and plain accesses that this replaces: 4.48 / 4.80.
+#ifndef DRAID_GFV_NTHR
+#define DRAID_GFV_NTHR 64
+#endif
+#ifndef DRAID_GFV_U
+#define DRAID_GFV_U 1
+#endif
+#ifndef DRAID_GFV_POL
+#define DRAID_GFV_POL pol_aux(2, 18)
+#endif
+template <class T, int NTHR, int U, int POL>
+__global__ __launch_bounds__(NTHR) void k_gf_vect_mul(const uint8_t* src, uint8_t* dst,
+                                                      uint32_t len, T t)
 {
-    const uint32_t tid = blockIdx.x * kThreads + threadIdx.x;
-    const uint32_t nth = gridDim.x * kThreads;
+    constexpr uint32_t VPB = static_cast<uint32_t>(NTHR) * U;  // vectors per workgroup
+    const uint32_t tid = threadIdx.x;
     if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
         const uint32_t nvec = len >> 4;
-        for (uint32_t i = tid; i < nvec; i += nth)
-            Mem<u32x4>::st<0>(dst, i, gf_mulc(t, Mem<u32x4>::ld<0>(src, i)));
-        for (uint32_t b = nvec * 16 + tid; b < len; b += nth)
-            Mem<uint32_t>::st<0>(dst, b, gf_mulc(t, Mem<uint32_t>::ld<0>(src, b)));
+        const uint32_t i0 = blockIdx.x * VPB + tid;
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = i0 + u * NTHR < nvec ? Mem<u32x4>::ld<POL>(src, i0 + u * NTHR) : u32x4(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * NTHR < nvec)
+                Mem<u32x4>::st<POL>(dst, i0 + u * NTHR, gf_mulc(t, v[u]));
+        const uint32_t tail = len & 15u;  // the last workgroup also owns the ragged bytes
+        if (tail && blockIdx.x == gridDim.x - 1 && tid < tail)
+            Mem<uint32_t>::st<0>(dst, nvec * 16 + tid,
+                                 gf_mulc(t, Mem<uint32_t>::ld<0>(src, nvec * 16 + tid)));
     } else {
-        for (uint32_t b = tid; b < len; b += nth)
+        const uint32_t b1 = min(len, (blockIdx.x + 1) * VPB * 16u);
+        for (uint32_t b = blockIdx.x * VPB * 16u + tid; b < b1; b += NTHR)
             Mem<uint32_t>::st<0>(dst, b, gf_mulc(t, Mem<uint32_t>::ld<0>(src, b)));
     }
 }
@@ -2091,26 +2122,59 @@ hipError_t launch_update_work(uint32_t m, uint32_t nd, const uint8_t* const* tab
 #undef DRAID_UPD
 }
 
+// True when tbl (isa-l's 32-byte layout: c * i for i < 16, then c * (i << 4)) is a
+// linear map over GF(2) -- every entry the XOR of the entries of its set bits, as
+// in any table gf_vect_mul_init makes -- and then writes the products of the eight
+// basis bytes to p.  A caller may hand any 32 bytes; those that are not linear keep
+// isa-l's lookup semantics through the nibble tables.
+static bool nibble_table_is_linear(const uint8_t tbl[32], uint32_t p[8])
+{
+    for (int h = 0; h < 2; ++h) {
+        const uint8_t* t = tbl + 16 * h;
+        for (int i = 0; i < 16; ++i) {
+            uint8_t x = 0;
+            for (int b = 0; b < 4; ++b)
+                if (i & (1 << b))
+                    x ^= t[1 << b];
+            if (t[i] != x)
+                return false;
+        }
+        for (int b = 0; b < 4; ++b)
+            p[4 * h + b] = t[1 << b];
+    }
+    return true;
+}
+
 hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t* src,
                               uint8_t* dst, hipStream_t st)
 {
+    constexpr int NTHR = DRAID_GFV_NTHR, U = DRAID_GFV_U, POL = DRAID_GFV_POL;
     if (len == 0)
         return hipSuccess;
     if (len > kMaxStripLen)
         return hipErrorInvalidValue;
-    NibTable t;
-    for (int w = 0; w < 4; ++w) {
-        t.lo[w] = tbl[4 * w] | (tbl[4 * w + 1] << 8) | (tbl[4 * w + 2] << 16) |
-                  (static_cast<uint32_t>(tbl[4 * w + 3]) << 24);
-        t.hi[w] = tbl[16 + 4 * w] | (tbl[16 + 4 * w + 1] << 8) | (tbl[16 + 4 * w + 2] << 16) |
-                  (static_cast<uint32_t>(tbl[16 + 4 * w + 3]) << 24);
+    const uint64_t per_block = static_cast<uint64_t>(NTHR) * U * 16;
+    const dim3 grid(static_cast<uint32_t>((len + per_block - 1) / per_block));
+    uint32_t p[8];
+    if (nibble_table_is_linear(tbl, p)) {
+        MulTable t;
+        tri_words(p[0], p[1], p[2], t.t0);
+        tri_words(p[3], p[4], p[5], t.t1);
+        t.t2 = (p[6] << 8) | (p[7] << 16) | ((p[6] ^ p[7]) << 24);
+        hipLaunchKernelGGL((k_gf_vect_mul<MulTable, NTHR, U, POL>), grid, dim3(NTHR), 0, st, src,
+                           dst, static_cast<uint32_t>(len), t);
+    } else {
+        NibTable t;
+        for (int w = 0; w < 4; ++w) {
+            t.lo[w] = tbl[4 * w] | (tbl[4 * w + 1] << 8) | (tbl[4 * w + 2] << 16) |
+                      (static_cast<uint32_t>(tbl[4 * w + 3]) << 24);
+            t.hi[w] = tbl[16 + 4 * w] | (tbl[16 + 4 * w + 1] << 8) |
+                      (tbl[16 + 4 * w + 2] << 16) |
+                      (static_cast<uint32_t>(tbl[16 + 4 * w + 3]) << 24);
+        }
+        hipLaunchKernelGGL((k_gf_vect_mul<NibTable, NTHR, U, POL>), grid, dim3(NTHR), 0, st, src,
+                           dst, static_cast<uint32_t>(len), t);
     }
-    const uint64_t vec = (len + 15) / 16;
-    uint64_t blocks = (vec + kThreads - 1) / kThreads;
-    if (blocks > 4096)
-        blocks = 4096;
-    hipLaunchKernelGGL(k_gf_vect_mul, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, st,
-                       src, dst, static_cast<uint32_t>(len), t);
     return hipGetLastError();
 }
 

@@ -165,6 +165,35 @@ def test_gf_vect_mul_every_constant(ec):
     assert (host(d2[5:5 + L]) == ref).all()
 
 
+@pytest.mark.parametrize("L", [32, 4096 + 32, 3 * 4096 + 96, (1 << 20) + 64])
+def test_gf_vect_mul_any_table_any_length(ec, L):
+    """A table from gf_vect_mul_init is a linear map and takes the 3-bit-table kernel;
+    32 arbitrary bytes are not and must keep isa-l's two nibble lookups.  Lengths
+    below, across and far beyond one workgroup's share (multiples of 32, isa-l's
+    contract), from an unaligned address too."""
+    rng = np.random.default_rng(L)
+    src_np = rng.integers(0, 256, L, dtype=np.uint8)
+    src = dev(src_np)
+    ref = np.zeros(L, np.uint8)
+    tables = [np.frombuffer(ec.gf_vect_mul_init(0xA7), np.uint8).copy(),
+              rng.integers(0, 256, 32, dtype=np.uint8)]
+    almost = tables[0].copy()
+    almost[16 + 11] ^= 0x40          # linear but for one entry of the high half
+    tables.append(almost)
+    for tbl in tables:
+        dst = torch.full((L + 64,), 0xEE, dtype=torch.uint8, device=DEV)
+        assert ec.gf_vect_mul(L, tbl.tobytes(), src, dst[:L]) == 0
+        assert oracle.gf_vect_mul(L, tbl.copy(), src_np, ref) == 0
+        got = host(dst)
+        assert (got[:L] == ref).all()
+        assert (got[L:] == 0xEE).all()   # nothing written past the end
+        dst.fill_(0xEE)
+        assert ec.gf_vect_mul(L, tbl.tobytes(), src, dst[7:7 + L]) == 0
+        got = host(dst)
+        assert (got[7:7 + L] == ref).all()
+        assert (got[:7] == 0xEE).all() and (got[7 + L:] == 0xEE).all()
+
+
 @pytest.mark.parametrize("k,m", [(2, 1), (4, 1), (8, 1), (16, 1), (8, 2), (9, 2), (10, 2), (12, 2), (14, 2),
                                  (16, 2), (40, 2)])
 def test_recover_every_failure_set(ec, k, m):
