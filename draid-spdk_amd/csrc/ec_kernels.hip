@@ -936,8 +936,21 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
 // through LDS after one barrier.
 
 // Split kernels take a 2-D/3-D grid -- x the chunk, y (and z beyond 65535) the
-// stripe -- so an item's coordinates cost no division.
+// stripe -- so an item's coordinates cost no division.  A grid whose x extent is
+// tiny dispatches slowly (8+2 x 4 KiB strips, x = 4: 531 us per launch against 444
+// for the same items on a 1-D grid), so when a strip has fewer than 64 chunks and
+// their number is a power of two, 2^fold neighbouring stripes share one x row:
+// x = chunk | stripe_low << cshift.  Otherwise fold = 0 and cshift = 31 (x < 2^31,
+// so the same two shifts and the mask leave chunk = x, stripe_low = 0).
 constexpr uint32_t kGridY = 65535;
+struct ItemGrid {
+    uint32_t cshift, fold;
+    __device__ __forceinline__ void coords(uint32_t& c, uint32_t& s) const
+    {
+        c = blockIdx.x & ((1u << cshift) - 1u);
+        s = ((blockIdx.z * kGridY + blockIdx.y) << fold) + (blockIdx.x >> cshift);
+    }
+};
 
 template <int SPLIT>
 struct SplitLds {
@@ -1077,11 +1090,12 @@ __device__ __forceinline__ bool encode_item_split(const Ptrs& pp, uint32_t s, ui
 
 template <int KT, int M, bool CHECK, class C, class Ptrs>
 __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_split(
-    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, uint32_t* flag)
+    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, uint32_t* flag, ItemGrid ig)
 {
     static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one split item per workgroup, stripe order");
     __shared__ SplitLds<C::SPLIT> lds;
-    const uint32_t c = blockIdx.x, s = blockIdx.z * kGridY + blockIdx.y;
+    uint32_t c, s;
+    ig.coords(c, s);
     if (s >= nstripes)
         return;  // uniform: the ragged last z-slice
     const bool bad = encode_item_split<KT, M, CHECK, C>(pp, s, c, len, cps, lds);
@@ -1228,12 +1242,13 @@ __device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, Rec
 template <int KT, int M, class C, class Ptrs>
 __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_cols(
     Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, const uint8_t* fail, uint32_t f01,
-    uint32_t* bad)
+    uint32_t* bad, ItemGrid ig)
 {
     static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one shared item per workgroup, stripe order");
     constexpr int SPLIT = C::SPLIT, POL = C::POL;
     __shared__ ColLds<KT> lds;
-    const uint32_t c = blockIdx.x, s = blockIdx.z * kGridY + blockIdx.y;
+    uint32_t c, s;
+    ig.coords(c, s);
     if (s >= nstripes)
         return;
     const bool aligned = stripe_aligned<KT, M>(pp, s, KT);
@@ -1572,10 +1587,23 @@ static bool grid_for(uint64_t len, uint32_t nstripes, uint32_t& cps, uint32_t& g
     return true;
 }
 
-static inline dim3 split_grid(uint32_t cps, uint32_t nstripes)
+// log2 of the x extent that short strips are folded up to: 4, 6, 8 and 10 measure
+// the same (profiles/r02/split/short_strip_grid_fold_extent.jsonl).
+#ifndef DRAID_FOLD_LOG
+#define DRAID_FOLD_LOG 6
+#endif
+static inline dim3 split_grid(uint32_t cps, uint32_t nstripes, ItemGrid& ig)
 {
-    const uint32_t ny = nstripes < kGridY ? nstripes : kGridY;
-    return dim3(cps, ny, (nstripes + kGridY - 1) / kGridY);
+    ig = ItemGrid{31, 0};
+    if (cps < (1u << DRAID_FOLD_LOG) && (cps & (cps - 1)) == 0) {
+        uint32_t lc = 0;
+        while ((1u << lc) < cps)
+            ++lc;
+        ig = ItemGrid{lc, DRAID_FOLD_LOG - lc};
+    }
+    const uint32_t rows = (nstripes + (1u << ig.fold) - 1) >> ig.fold;
+    const uint32_t ny = rows < kGridY ? rows : kGridY;
+    return dim3(cps << ig.fold, ny, (rows + kGridY - 1) / kGridY);
 }
 
 template <int KT, int M, bool CHECK, class C, class Ptrs>
@@ -1587,11 +1615,12 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
         return hipSuccess;
     if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    if constexpr (C::SPLIT > 1)
-        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), split_grid(cps, nstripes),
-                           dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
-                           flag);
-    else if constexpr (KT > 0 && std::is_same<Ptrs, TablePtrs>::value)
+    if constexpr (C::SPLIT > 1) {
+        ItemGrid ig;
+        const dim3 g = split_grid(cps, nstripes, ig);
+        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
+                           static_cast<uint32_t>(len), cps, nstripes, flag, ig);
+    } else if constexpr (KT > 0 && std::is_same<Ptrs, TablePtrs>::value)
         hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), 0,
                            st, TablePlain{pp.tab, pp.stride}, k, static_cast<uint32_t>(len), cps,
                            nstripes, flag);
@@ -1610,13 +1639,15 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
         return hipSuccess;
     if (!grid_for<C>(len, nstripes, cps, grid))
         return hipErrorInvalidValue;
-    if constexpr (C::SPLIT > 1)
-        hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), split_grid(cps, nstripes),
-                           dim3(C::NTHR), 0, st, pp, static_cast<uint32_t>(len), cps, nstripes,
-                           fail, f01, bad);
-    else
+    if constexpr (C::SPLIT > 1) {
+        ItemGrid ig;
+        const dim3 g = split_grid(cps, nstripes, ig);
+        hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
+                           static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
+    } else {
         hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp,
                            k, static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
+    }
     return hipGetLastError();
 }
 

@@ -45,9 +45,9 @@ class Batch:
         else:
             self.view()[:, :, :L] = dev(data)
         base = self.buf.data_ptr() + offset
-        ptrs = [base + s * self.stripe_stride + j * self.strip_stride
-                for s in range(B) for j in range(k + m)]
-        self.table = torch.tensor(ptrs, dtype=torch.int64, device=DEV)
+        ptrs = (base + np.arange(B, dtype=np.int64)[:, None] * self.stripe_stride +
+                np.arange(k + m, dtype=np.int64)[None, :] * self.strip_stride)
+        self.table = torch.from_numpy(ptrs.reshape(-1)).to(DEV)
 
     def view(self):
         return self.buf[self.offset:self.offset + self.B * self.stripe_stride].view(
@@ -569,10 +569,31 @@ def test_shared_items_every_length_class(ec, k, m):
             assert (host(b.view()[:, :, L:]) == 0).all()
 
 
-@pytest.mark.parametrize("k,m,L,B", [(8, 2, 64, 70000), (16, 2, 32, 66000), (4, 1, 64, 66000)])
+def _random_failures_vec(rng, B, k, m):
+    """_random_failures without the per-stripe Python loop, for very long batches."""
+    f = np.full((B, 2), 0xFF, np.uint8)
+    x = rng.integers(0, k, B)
+    y = (x + 1 + rng.integers(0, k - 1, B)) % k if k > 1 else x
+    kind = rng.integers(0, 6, B) if m == 2 else np.zeros(B, np.int64)
+    f[:, 0] = np.where(kind == 5, k, np.where(kind == 4, k + 1, x))
+    if m == 1:
+        f[:, 0] = rng.integers(0, k + 1, B)
+        return f
+    f[:, 1] = np.where(kind == 0, 0xFF,
+                       np.where(kind <= 2, y, np.where(kind == 3, k, np.where(kind == 4, x, k + 1))))
+    return f
+
+
+@pytest.mark.parametrize("k,m,L,B", [
+    (8, 2, 64, 70000), (16, 2, 32, 66000), (4, 1, 64, 66000),   # short strips: stripes share grid rows
+    (8, 2, 2049, 66000),                  # three chunks per strip: one stripe per row, z > 1
+    (3, 1, 16, 64 * 65535 + 77),          # 64 stripes per row and still more rows than one z slice
+    (8, 2, 16, 64 * 65535 + 77),
+])
 def test_more_stripes_than_one_grid_row(ec, k, m, L, B):
-    """More than 65535 stripes: the shared-item kernels index stripes through the
-    second and third grid dimensions."""
+    """The shared-item kernels index chunks and stripes through the three grid
+    dimensions: stripes of short strips share an x row, and more than 65535 rows
+    spill into z."""
     stream = torch.cuda.current_stream().cuda_stream
     rng = np.random.default_rng(B)
     b = Batch(k, m, L, B, seed=B)
@@ -581,7 +602,8 @@ def test_more_stripes_than_one_grid_row(ec, k, m, L, B):
     sync()
     good = host(b.strips())
     assert (good == oracle_encode(before, k, m)).all()
-    fail = _random_failures(rng, B, k, m)
+    del before
+    fail = _random_failures_vec(rng, B, k, m)
     lost = torch.from_numpy(fail.astype(np.int64)).to(DEV)
     v = b.strips()
     rows = torch.arange(B, device=DEV)
