@@ -646,7 +646,10 @@ __device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k,
         if (!ok[u])
             continue;
         const uint32_t i = i0 + u * stride;
-        if (pl.nd == 0) {
+        if constexpr (M == 1) {
+            // RAID5: the one lost strip (data or P) is the XOR of the survivors
+            MW::template st<POL>(pl.nd == 0 ? pP : pX, i, pv[u] ^ ps[u]);
+        } else if (pl.nd == 0) {
             if (pl.lostP)
                 MW::template st<POL>(pP, i, ps[u]);
             if (M == 2 && pl.lostQ)
@@ -852,7 +855,7 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
     if constexpr (C::MAP == 2)
         stage_gf_tables<C::NTHR>(lds);  // once per persistent workgroup
     TabStage<C::NTHR> tabs;
-    if constexpr (C::MAP != 2 && C::PLAN == 0)
+    if constexpr (M == 2 && C::MAP != 2 && C::PLAN == 0)
         tabs.load();
     for (uint32_t b = blockIdx.x; b < total; b += (C::MAP == 2 ? gridDim.x : total)) {
         uint32_t s, c;
@@ -887,7 +890,10 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
                 atomicAdd(bad, 1u);
             continue;  // uniform across the workgroup
         }
-        if constexpr (C::PLAN == 2 || C::PLAN == 3) {
+        if constexpr (M == 1) {
+            // RAID5 rebuilds by XOR alone: no constants, no tables, no barrier
+            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [](RecPlan&) {});
+        } else if constexpr (C::PLAN == 2 || C::PLAN == 3) {
             // DIAGNOSTIC ONLY (tools/sweep.py): constants left zero, no LDS, no
             // barrier -- wrong results, measures what the plan step costs.
             reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
@@ -1170,9 +1176,11 @@ __device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, Rec
             lds.row[KT + 1][lane] = qv;
         return PartPQ{};
     });
-    const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
-    pl.t1 = mul.t1;
-    pl.t2 = mul.t2;
+    if constexpr (M == 2) {
+        const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
+        pl.t1 = mul.t1;
+        pl.t2 = mul.t2;
+    }
     __syncthreads();
     // phase 2: this wave's columns, all strips
     constexpr int ND = 4 / SPLIT;
@@ -1205,7 +1213,9 @@ __device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, Rec
     if (!okw)
         return;
     uint32_t o1[ND], o2[ND];
-    if (pl.nd == 0) {
+    if constexpr (M == 1) {
+        st_words<POL, ND>(pl.nd == 0 ? pP : pX, ob, pt);  // RAID5: XOR of the survivors
+    } else if (pl.nd == 0) {
         if (pl.lostP)
             st_words<POL, ND>(pP, ob, pt);
         if (M == 2 && pl.lostQ)
@@ -1371,7 +1381,8 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_w
     constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
     const int k = KT > 0 ? KT : static_cast<int>(k_rt);
     TabStage<C::NTHR> tabs;
-    tabs.load();
+    if constexpr (M == 2)
+        tabs.load();
     for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
         uint32_t seg, chunk, len, cps;
         ws.get(b, CB, seg, chunk, len, cps);
@@ -1379,10 +1390,14 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_w
         RecPlan pl = decode_failures<M>(k, f[0], f[1]);
         if (pl.skip)
             continue;
-        reconstruct_item<KT, M, C>(pp, seg, chunk, k, len, cps, pl, [&](RecPlan& p) {
-            tabs.store(lds);
-            plan_constants(p, l_exp, l_log);
-        });
+        if constexpr (M == 1) {
+            reconstruct_item<KT, M, C>(pp, seg, chunk, k, len, cps, pl, [](RecPlan&) {});
+        } else {
+            reconstruct_item<KT, M, C>(pp, seg, chunk, k, len, cps, pl, [&](RecPlan& p) {
+                tabs.store(lds);
+                plan_constants(p, l_exp, l_log);
+            });
+        }
     }
 }
 
@@ -1696,12 +1711,22 @@ constexpr int kLanes = 64;
 #define DRAID_REC_WAVES -1
 #endif
 constexpr int enc_waves(int k) { return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES : k <= 4 ? 7 : 6; }
+// The RAID5 (m = 1) one-wave reconstruct is XOR only -- no tables, no LDS, no
+// barrier -- and has optima of its own (profiles/r02/occupancy/
+// raid5_reconstruct_waves.jsonl, us per launch): 3+1 390 at 5 vs 402 at the
+// compiler's choice, 4+1 201.7 at 4 vs 204-208, 5+1 398.7 at 4 vs 407 at 5, 7+1 403
+// at 3 vs 411 at 4; 2+1 is best left to the compiler (396 vs 420 at 5).
+constexpr int rec_waves_raid5(int k)
+{
+    return k <= 2 ? 0 : k == 3 ? 5 : k <= 6 ? 4 : k == 7 ? 3 : k <= 12 ? 4 : 3;
+}
 constexpr int rec_waves(int k, int m)
 {
     return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
+           : m == 1             ? rec_waves_raid5(k)
            : k <= 4             ? 0
-           : k == 5             ? (m == 2 ? 6 : 5)
-           : k == 6             ? (m == 2 ? 5 : 4)
+           : k == 5             ? 6
+           : k == 6             ? 5
            : k <= 12            ? 4
                                 : 3;
 }
