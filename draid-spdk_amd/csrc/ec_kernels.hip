@@ -1783,6 +1783,8 @@ constexpr int rec_split_waves(int k, int m)
     return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
            : rec_split(k) == 1  ? rec_waves(k, m)
            : (k == 8 && m == 2) ? 6
+           : (k == 16 && m == 1) ? 3  // 398 vs 404 us at 4
+           : k >= 15             ? 4  // (k + 2) KiB of LDS per item leave room for no more
                                 : 5;
 }
 template <int U, int MAP = 0, int WAVES = 0, int SPLIT = 1>
