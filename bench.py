@@ -37,7 +37,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 
 
 def shard_range(nstripes_total: int, rank: int, world: int) -> tuple[int, int]:
-    """Contiguous stripe range [lo, hi) of a rank."""
+    """Contiguous stripe range [lo, hi) of a rank: stripes are independent, so ranks shard them
+    with no collective on the data path."""
     return nstripes_total * rank // world, nstripes_total * (rank + 1) // world
 
 
@@ -71,7 +72,7 @@ def failure_single(nstripes: int, k: int, seed: int) -> np.ndarray:
 
 # BASELINE.json configs the harness can run.  The default (no --config) is the
 # headline metric's workload; the others are measured with the same harness and
-# recorded in DESIGN.md (they are not the driver's bench line).
+# reported beside it (they are not the driver's bench line).
 CONFIGS = {
     # configs[2] -- the metric's workload: RAID6 8+2 encode + reconstruct at 64 KiB
     "raid6_8p2_64k": dict(k=8, m=2, strip_kib=64, stripes=4096, failures="dual",
@@ -82,7 +83,7 @@ CONFIGS = {
                           label="RAID5 4+1 XOR encode + single-failure reconstruct, 64 KiB "
                                 "strips (configs[1])"),
     # configs[3] -- RAID6 8+2 single-failure degraded read, 128 KiB; strong scaling
-    # (--strong) splits 16384 stripes (20 GiB) over the ranks (SURVEY.md §8d)
+    # (--strong) splits 16384 stripes (20 GiB) over the ranks
     "raid6_8p2_128k_single": dict(k=8, m=2, strip_kib=128, stripes=4096, strong_stripes=16384,
                                   failures="single",
                                   label="RAID6 8+2 encode + single-failure reconstruct, 128 KiB "
@@ -96,7 +97,8 @@ CONFIGS = {
 
 
 def reconstruct_bytes_per_stripe(k: int, m: int, S: int, failures: str) -> int:
-    """Algorithmic HBM bytes of one stripe's reconstruct."""
+    """Algorithmic HBM bytes of one stripe's reconstruct: every surviving strip it needs is
+    read once, every lost strip written once."""
     if failures == "dual":
         return (k + 2) * S          # k-2 data + P + Q read, 2 written
     return (k + 1) * S              # k-1 data + P read, 1 written
@@ -301,7 +303,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--layout", default="stripe_major", choices=["stripe_major", "strip_major"],
-                    help="placement of the stripes in HBM (DESIGN.md §3)")
+                    help="placement of the stripes in HBM: stripe-major (one stripe-cache slot per "
+                         "stripe) or strip-major (one region per strip index)")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--stripe-pad", type=int, default=0,
                     help="lab runs only: bytes added to the stripe pitch of the stripe-major layout "
@@ -354,7 +357,7 @@ def main() -> None:
         cfg = dict(k=int(sk), m=int(sm), strip_kib=int(skib), stripes=int(sb), failures=sf,
                    label=f"lab shape {sk}+{sm} x {skib} KiB, {sf} failure")
     k, m, S = cfg["k"], cfg["m"], cfg["strip_kib"] * 1024
-    if args.strong:  # fixed total, contiguous stripe ranges per rank (SURVEY.md §8e)
+    if args.strong:  # fixed total, contiguous stripe ranges per rank
         total = args.stripes or cfg.get("strong_stripes", cfg["stripes"])
     else:            # weak scaling: B stripes per GPU
         total = (args.stripes or cfg["stripes"]) * world
@@ -498,7 +501,7 @@ def main() -> None:
         "breakdown": {
             "encode_ms": round(enc_ms, 4),
             "reconstruct_ms": round(rec_ms, 4),
-            "encode_ms_median": round(float(np.median(enc_all)), 4),
+            "encode_ms_median": round(float(np.median(enc_all)), 4),  # medians beside the means: a slow start does not hide
             "reconstruct_ms_median": round(float(np.median(rec_all)), 4),
             "encode_user_gib_s": round(k * S * B / (enc_ms * 1e-3) / GIB, 1),
             "reconstruct_user_gib_s": round(k * S * B / (rec_ms * 1e-3) / GIB, 1),

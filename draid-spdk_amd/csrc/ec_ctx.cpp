@@ -180,7 +180,7 @@ namespace {
 
 // Address order.  A batch whose stripes sit at scattered addresses (stripe-cache
 // slots or user buffers taken out of order) runs 7-11% slower than the same
-// stripes visited in address order (locality at tens-of-MiB
+// stripes visited in address order (measured: locality at tens-of-MiB
 // scale), so a group whose segments jump back in memory is launched sorted by
 // the address of their first strip -- a stable counting sort into at most 4096
 // buckets (>= 1 MiB each) over the group's address range, O(segments).

@@ -2,7 +2,7 @@
 //
 // Field: GF(2^8) / x^8+x^4+x^3+x^2+1 (0x11D), generator 2 -- the field isa-l
 // v2.30 uses for pq_gen / gf_mul (reference call sites:
-// examples/bdev/gf_vect_mul/gf_vect_mul.c:60-66,101,267; SURVEY.md App. A).
+// examples/bdev/gf_vect_mul/gf_vect_mul.c:60-66,101,267).
 //
 // Everything here is byte-parallel integer work on 32-bit VALU lanes: no MFMA.
 #pragma once

@@ -1,7 +1,7 @@
 // ec_kernels.hip -- RAID5 XOR / RAID6 P+Q encode and reconstruct kernels for
 // MI355X (gfx950, CDNA4).
 //
-// Hot path (SURVEY.md §8a): the full-stripe parity of
+// Hot path: the full-stripe parity of
 //   raid5_stripe_write_preread_complete  module/bdev/raid/raid5.c:743-777
 //   raid5_xor_stripe                     module/bdev/raid/raid5_simple.c:141-203
 //   pq_gen                               examples/bdev/gf_vect_mul/gf_vect_mul.c:101
@@ -25,11 +25,14 @@
 #include "ec_gf.hpp"
 #include "ec_launch.hpp"
 
+// the kernels, in dependency order
+#include "kern_mem.hpp"
+#include "kern_cfg.hpp"
+#include "kern_encode.hpp"
+#include "kern_reconstruct.hpp"
+#include "kern_worklist.hpp"
+
 namespace draid {
-
-constexpr int kThreads = 256;
-
-__constant__ GfTables c_gf = make_gf_tables();
 
 #ifndef DRAID_EC_LAB
 #define DRAID_EC_LAB 0
@@ -38,1521 +41,6 @@ __constant__ GfTables c_gf = make_gf_tables();
 static int g_variant = 0;
 void set_variant(int v) { g_variant = DRAID_EC_LAB ? v : 0; }
 int get_variant() { return g_variant; }
-
-// ------------------------------------------------------------ pointers
-
-// AS4: read the table through the constant address space.  The table is input
-// only, and a constant-space read at a wave-uniform index is always a scalar load
-// (an ordinary global read becomes a per-lane load as soon as any store, atomic,
-// LDS write or barrier precedes it, and its pointer then lives in VGPRs).  The
-// split kernels and every reconstruct need that; the one-wave encode (k = 2, the
-// runtime-k fallback, the check kernels) ran 2% faster on ordinary reads (4+1 x
-// 64 KiB 203.2 vs 207.4 us), which the compiler already turns into scalar loads
-// there.
-#ifndef DRAID_KEEP_POINTERS
-#define DRAID_KEEP_POINTERS 1
-#endif
-template <bool AS4>
-struct TablePtrsT {
-    const uint8_t* const* tab;
-    uint32_t stride;
-    __device__ __forceinline__ const uint8_t* get(uint32_t s, int j) const
-    {
-        if constexpr (AS4) {
-            typedef const uint8_t* const __attribute__((address_space(4)))* ctab;
-            const uint8_t* p = ((ctab)(uintptr_t)tab)[(size_t)s * stride + j];
-#if DRAID_KEEP_POINTERS
-            // Opaque to the register allocator: a constant-space load is trivially
-            // rematerialisable, and under SGPR pressure the compiler re-read the whole
-            // pointer row (s_load_dwordx16 + wait) in front of EVERY strip load of
-            // the one-wave reconstruct, serialising the loads behind scalar round trips.
-            asm("" : "+s"(p));
-#endif
-            return p;
-        } else {
-            return tab[(size_t)s * stride + j];
-        }
-    }
-};
-#if defined(DRAID_TABLE_PLAIN)
-using TablePtrs = TablePtrsT<false>;
-#else
-using TablePtrs = TablePtrsT<true>;
-#endif
-using TablePlain = TablePtrsT<false>;
-
-// Regular layout: strip j of stripe s at base + s*stripe_stride + j*strip_stride
-// (a stripe cache laid out as one array, or pinned host stripes read in place).
-struct StridedPtrs {
-    const uint8_t* base;
-    uint64_t strip_stride, stripe_stride;
-    __device__ __forceinline__ const uint8_t* get(uint32_t s, int j) const
-    {
-        return base + s * stripe_stride + static_cast<uint64_t>(j) * strip_stride;
-    }
-};
-
-struct ArgPtrs {
-    ArgPtrTable t;
-    __device__ __forceinline__ const uint8_t* get(uint32_t, int j) const { return t.p[j]; }
-};
-
-// ------------------------------------------------------------ memory words
-
-// Strip pointers come from a table of generic pointers; casting to the global
-// address space lets the compiler emit global_load/store with the uniform strip
-// base in SGPRs and a 32-bit per-lane offset (saddr + voffset form) instead of
-// flat instructions with 64-bit per-lane addresses.
-typedef const u32x4 __attribute__((address_space(1)))* gcv4;
-typedef u32x4 __attribute__((address_space(1)))* gv4;
-typedef const uint8_t __attribute__((address_space(1)))* gcb;
-typedef uint8_t __attribute__((address_space(1)))* gb;
-
-// W = u32x4: one 16-byte vector, index in vectors.  W = uint32_t: one byte
-// held in the low 8 bits, index in bytes (tails and unaligned strips).
-// Indices are 32-bit: strips are < 4 GiB (checked on the host).
-//
-// POL (cache policy of the 16-byte accesses): bit 0 non-temporal loads, bit 1
-// non-temporal stores (global instructions).  Bits 8..15 / 16..23 select
-// buffer instructions instead, with explicit gfx950 cache-policy bits
-// (aux = sc0 1 | nt 2 | sc1 16): load aux + 1 / store aux + 1 (0 = global form).
-// The production policies (EncCfg / RecCfg below) are two of these.
-constexpr int pol_aux(int load_aux, int store_aux)
-{
-    return 3 | ((load_aux + 1) << 8) | ((store_aux + 1) << 16);
-}
-
-// 1: the shared-item reconstruct loads a strip it skips (lost, or not needed)
-// through a descriptor with no records instead of branching around the load
-// (Mem<u32x4>::ld_if): 16+2 x 256 KiB dual 380 vs 389 us.  The one-wave
-// reconstruct keeps its uniform branches -- there the same change is neutral to
-// 1% slower (8+2 x 128 KiB single 377.6 vs 374.1, 4+1 207.6 vs 204.0).  0 for A/B.
-#ifndef DRAID_DEAD_LOADS
-#define DRAID_DEAD_LOADS 1
-#endif
-
-template <class W>
-struct Mem;
-
-template <>
-struct Mem<u32x4> {
-    static __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* p)
-    {
-        // p is wave-uniform (a strip base), so the descriptor lives in SGPRs
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, 0x7fffffff,
-                                                 0x00020000);
-    }
-    template <int POL>
-    static __device__ __forceinline__ u32x4 ld(const uint8_t* p, uint32_t i)
-    {
-        constexpr int aux = (POL >> 8) & 0xff;
-        if constexpr (aux != 0)
-            return __builtin_amdgcn_raw_buffer_load_b128(rsrc(p), static_cast<int>(i << 4), 0,
-                                                         aux - 1);
-        gcv4 q = (gcv4)(p + (i << 4));
-        if constexpr ((POL & 1) != 0)
-            return __builtin_nontemporal_load(q);
-        else
-            return *q;
-    }
-    // Loads vector i when `live` (wave-uniform), zeros otherwise.  Through a buffer
-    // descriptor a dead load is one with no records -- it returns zeros without
-    // touching memory -- so a skipped strip costs neither a branch nor the moves
-    // that zero its registers.
-    template <int POL>
-    static __device__ __forceinline__ u32x4 ld_if(const uint8_t* p, uint32_t i, bool live)
-    {
-        constexpr int aux = (POL >> 8) & 0xff;
-        if constexpr (aux != 0 && DRAID_DEAD_LOADS) {
-            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint8_t*>(p), 0, live ? 0x7fffffff : 0, 0x00020000);
-            return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(i << 4), 0, aux - 1);
-        } else {
-            return live ? ld<POL>(p, i) : u32x4(0);
-        }
-    }
-    template <int POL>
-    static __device__ __forceinline__ void st(const uint8_t* p, uint32_t i, u32x4 v)
-    {
-        constexpr int aux = (POL >> 16) & 0xff;
-        if constexpr (aux != 0) {
-            __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(p), static_cast<int>(i << 4), 0,
-                                                   aux - 1);
-            return;
-        }
-        gv4 q = (gv4)(const_cast<uint8_t*>(p) + (i << 4));
-        if constexpr ((POL & 2) != 0)
-            __builtin_nontemporal_store(v, q);
-        else
-            *q = v;
-    }
-    static __device__ __forceinline__ bool any(u32x4 v) { return (v.x | v.y | v.z | v.w) != 0; }
-};
-
-template <>
-struct Mem<uint32_t> {
-    template <int POL>
-    static __device__ __forceinline__ uint32_t ld(const uint8_t* p, uint32_t i)
-    {
-        return *((gcb)p + i);
-    }
-    template <int POL>
-    static __device__ __forceinline__ uint32_t ld_if(const uint8_t* p, uint32_t i, bool live)
-    {
-        return live ? ld<POL>(p, i) : 0u;
-    }
-    template <int POL>
-    static __device__ __forceinline__ void st(const uint8_t* p, uint32_t i, uint32_t v)
-    {
-        *((gb)const_cast<uint8_t*>(p) + i) = static_cast<uint8_t>(v);
-    }
-    static __device__ __forceinline__ bool any(uint32_t v) { return (v & 0xffu) != 0; }
-};
-
-// ND (1 or 2) consecutive dwords at a byte offset, with the store policy of POL.
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-template <int POL, int ND>
-__device__ __forceinline__ void st_words(const uint8_t* p, uint32_t byte_off,
-                                         const uint32_t (&v)[ND])
-{
-    static_assert(ND == 1 || ND == 2, "a dword or a pair");
-    constexpr int aux = (POL >> 16) & 0xff;
-    if constexpr (aux != 0) {
-        if constexpr (ND == 1)
-            __builtin_amdgcn_raw_buffer_store_b32(v[0], Mem<u32x4>::rsrc(p),
-                                                  static_cast<int>(byte_off), 0, aux - 1);
-        else
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, Mem<u32x4>::rsrc(p),
-                                                  static_cast<int>(byte_off), 0, aux - 1);
-    } else {
-        typedef uint32_t __attribute__((address_space(1)))* gw;
-        gw q = (gw)(const_cast<uint8_t*>(p) + byte_off);
-#pragma unroll
-        for (int n = 0; n < ND; ++n) {
-            if constexpr ((POL & 2) != 0)
-                __builtin_nontemporal_store(v[n], q + n);
-            else
-                q[n] = v[n];
-        }
-    }
-}
-
-// Calls f(j) for j = k-1 down to 0; fully unrolled when k is a template constant.
-template <int KT, class F>
-__device__ __forceinline__ void for_sources_desc(int k, F&& f)
-{
-    if constexpr (KT > 0) {
-#pragma unroll
-        for (int j = KT - 1; j >= 0; --j)
-            f(j);
-    } else {
-        for (int j = k - 1; j >= 0; --j)
-            f(j);
-    }
-}
-
-// Run-time stripe width (k without an unrolled instance): the strips in blocks of
-// kRtBlock, from the top down, every load of a block issued before the block's
-// arithmetic -- a plain loop over j would wait for each strip before asking for
-// the next.  The top block may reach past strip k-1: those slots load nothing
-// (ld_if with live == false, through the pointer of strip k-1, never one past the
-// row) and hand zeros to acc, which a Horner chain that is still zero ignores.
-// live(j): wave-uniform, false for a strip that must not be read.
-constexpr int kRtBlock = 8;
-template <int U, int POL, class W, class Ptrs, class Live, class Acc>
-__device__ __forceinline__ void for_blocks_desc(const Ptrs& pp, uint32_t s, int k,
-                                                const bool (&ok)[U], uint32_t i0,
-                                                uint32_t stride, Live&& live, Acc&& acc)
-{
-    using MW = Mem<W>;
-    for (int jb = ((k + kRtBlock - 1) / kRtBlock) * kRtBlock; jb > 0; jb -= kRtBlock) {
-        W d[kRtBlock][U];
-#pragma unroll
-        for (int t = kRtBlock - 1; t >= 0; --t) {
-            const int j = jb - kRtBlock + t;
-            const bool on = j < k && live(j);
-            const uint8_t* src = pp.get(s, j < k ? j : k - 1);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                d[t][u] = ok[u] ? MW::template ld_if<POL>(src, i0 + u * stride, on) : W(0);
-        }
-#pragma unroll
-        for (int t = kRtBlock - 1; t >= 0; --t)
-            acc(d[t]);
-    }
-}
-
-// ------------------------------------------------------------ encode core
-
-// Computes P (and Q for M == 2) over the U elements i0 + u*stride (< n) and
-// either stores them (CHECK == false) or compares them with the stored parity.
-// BOUNDED == false: the caller guarantees every element is in range (full
-// chunks), so no load or store is predicated.
-template <int KT, int M, int U, int POL, bool CHECK, bool BOUNDED, class W, class Ptrs>
-__device__ __forceinline__ bool encode_elems(const Ptrs& pp, uint32_t s, int k, uint32_t i0,
-                                             uint32_t stride, uint32_t n)
-{
-    using MW = Mem<W>;
-    W p[U], q[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        ok[u] = !BOUNDED || i0 + u * stride < n;
-        p[u] = W(0);
-        q[u] = W(0);
-    }
-    if constexpr (KT > 0) {
-        for_sources_desc<KT>(k, [&](int j) {
-            const uint8_t* src = pp.get(s, j);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const W d = ok[u] ? MW::template ld<POL>(src, i0 + u * stride) : W(0);
-                p[u] ^= d;
-                if constexpr (M == 2)
-                    q[u] = gf_mul2(q[u]) ^ d;
-            }
-        });
-    } else {
-        for_blocks_desc<U, POL, W>(
-            pp, s, k, ok, i0, stride, [](int) { return true; },
-            [&](const W(&d)[U]) __attribute__((always_inline)) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    p[u] ^= d[u];
-                    if constexpr (M == 2)
-                        q[u] = gf_mul2(q[u]) ^ d[u];
-                }
-            });
-    }
-    const uint8_t* dp = pp.get(s, k);
-    const uint8_t* dq = (M == 2) ? pp.get(s, k + 1) : nullptr;
-    bool bad = false;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if (!ok[u])
-            continue;
-        const uint32_t i = i0 + u * stride;
-        if constexpr (CHECK) {
-            bad |= MW::any(MW::template ld<0>(dp, i) ^ p[u]);
-            if constexpr (M == 2)
-                bad |= MW::any(MW::template ld<0>(dq, i) ^ q[u]);
-        } else {
-            MW::template st<POL>(dp, i, p[u]);
-            if constexpr (M == 2)
-                MW::template st<POL>(dq, i, q[u]);
-        }
-    }
-    return bad;
-}
-
-template <int KT, int M, class Ptrs>
-__device__ __forceinline__ bool stripe_aligned(const Ptrs& pp, uint32_t s, int k)
-{
-    uintptr_t acc = 0;
-    if constexpr (KT > 0) {
-#pragma unroll
-        for (int j = 0; j < KT + M; ++j)
-            acc |= reinterpret_cast<uintptr_t>(pp.get(s, j));
-    } else {
-        for (int j = 0; j < k + M; ++j)
-            acc |= reinterpret_cast<uintptr_t>(pp.get(s, j));
-    }
-    return (acc & 15u) == 0;
-}
-
-// Launch configuration knobs (A/B-tested with tools/sweep.py):
-//   NTHR  lanes per workgroup           U    16-B vectors per lane per strip
-//   POL   bit0 nt loads, bit1 nt stores
-//   MAP   0: block b -> (stripe b / cps, chunk b % cps)
-//         1: chunk-major (chunk b / nstripes, stripe b % nstripes)
-//         2: persistent grid-stride over stripe-major items
-//   PLAN  (one-wave reconstruct) 0: exp/log tables staged in LDS, 1: scalar reads of
-//         the __constant__ tables (no LDS, no barrier)
-//   WAVES waves per SIMD the kernel is built for (0: the compiler's choice).
-//         The compiler pads the register allocation so exactly this many waves
-//         fit: fewer resident waves keep fewer DRAM pages open at once, which
-//         is worth more to these streaming kernels than the extra latency
-//         hiding (8+2 x 64 KiB dual reconstruct: 0.411 ms at 5 waves, 0.420 at
-//         the 7 its 70 VGPRs would allow, 0.417 at 4).
-//   SPLIT waves that share one item: the workgroup has SPLIT * 64 lanes, the item
-//         is still 64 lanes wide (1 KiB of every strip at U = 1), and wave w loads
-//         only strips [w*KW, (w+1)*KW), KW = ceil(k / SPLIT); the encode's partial
-//         sums (k_encode_split) or the reconstruct's raw strips (k_reconstruct_cols)
-//         meet in LDS.  NTHR_ counts the lanes of the whole workgroup.
-template <int NTHR_, int U_, int POL_, int MAP_, int PLAN_ = 0, int WAVES_ = 0, int SPLIT_ = 1>
-struct Cfg {
-    static constexpr int NTHR = NTHR_, U = U_, POL = POL_, MAP = MAP_, PLAN = PLAN_,
-                         WAVES = WAVES_, SPLIT = SPLIT_, ITEM = NTHR_ / SPLIT_;
-    static_assert(SPLIT_ == 1 || (NTHR_ == 64 * SPLIT_ && U_ == 1), "a split item is one wave wide");
-};
-#define DRAID_WAVES_PER_EU(C) \
-    __attribute__((amdgpu_waves_per_eu((C::WAVES) ? (C::WAVES) : 1, (C::WAVES) ? (C::WAVES) : 8)))
-
-template <class C>
-__device__ __forceinline__ void item_coords(uint32_t b, uint32_t cps, uint32_t nstripes,
-                                            uint32_t& s, uint32_t& c)
-{
-    if constexpr (C::MAP == 1) {
-        c = b / nstripes;
-        s = b - c * nstripes;
-    } else if constexpr (C::MAP == 3) {
-        // XCD-aware: the dispatcher deals workgroup b to XCD b % 8; give each XCD a
-        // contiguous run of items (whole stripes) instead of every 8th chunk.
-        const uint32_t total = cps * nstripes, q = total >> 3, r = total & 7u;
-        const uint32_t x = b & 7u, i = b >> 3;
-        const uint32_t bb = x * q + min(x, r) + i;
-        s = bb / cps;
-        c = bb - s * cps;
-    } else if constexpr (C::MAP >= 4 && C::MAP <= 7) {
-        // Groups of G stripes swept together (lab study): consecutive workgroups
-        // take G different stripes; MAP 4/6 also skew each stripe's chunk by
-        // s_local * cps / G ("diagonal"), MAP 5/7 keep the same chunk (group
-        // chunk-major).  A ragged last group falls back to stripe order.
-        constexpr uint32_t G = (C::MAP == 4 || C::MAP == 5) ? 16u : 4u;
-        constexpr bool diag = (C::MAP == 4 || C::MAP == 6);
-        const uint32_t per_group = G * cps, g = b / per_group;
-        if ((g + 1) * G <= nstripes) {
-            const uint32_t i = b - g * per_group, sl = i % G, cc = i / G;
-            s = g * G + sl;
-            c = diag ? (cc + sl * (cps / G)) % cps : cc;
-        } else {
-            s = b / cps;
-            c = b - s * cps;
-        }
-    } else {
-        s = b / cps;
-        c = b - s * cps;
-    }
-}
-
-// One work item = chunk c (NTHR*U vectors) of every strip of stripe s.
-template <int KT, int M, bool CHECK, class C, class Ptrs>
-__device__ __forceinline__ bool encode_item(const Ptrs& pp, uint32_t s, uint32_t c, int k,
-                                            uint32_t len, uint32_t cps)
-{
-    constexpr int NTHR = C::NTHR, U = C::U, POL = C::POL;
-    constexpr uint32_t EPB = static_cast<uint32_t>(NTHR) * U;  // vectors per item
-    const uint32_t nvec = len >> 4;
-    bool bad = false;
-    if (stripe_aligned<KT, M>(pp, s, k)) {
-        const uint32_t i0 = c * EPB + threadIdx.x;
-        if ((c + 1) * EPB <= nvec)
-            bad = encode_elems<KT, M, U, POL, CHECK, false, u32x4>(pp, s, k, i0, NTHR, nvec);
-        else
-            bad = encode_elems<KT, M, U, POL, CHECK, true, u32x4>(pp, s, k, i0, NTHR, nvec);
-        const uint32_t tail = len & 15u;
-        if (tail && c == cps - 1 && threadIdx.x < tail)
-            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(
-                pp, s, k, nvec * 16 + threadIdx.x, NTHR, len);
-    } else {
-        const uint32_t b1 = min(len, (c + 1) * EPB * 16);
-        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += NTHR)
-            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(pp, s, k, b, NTHR, b1);
-    }
-    return bad;
-}
-
-template <int KT, int M, bool CHECK, class C, class Ptrs>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode(Ptrs pp, uint32_t k_rt, uint32_t len,
-                                                    uint32_t cps, uint32_t nstripes,
-                                                    uint32_t* flag)
-{
-    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
-    const uint32_t total = cps * nstripes;
-    bool bad = false;
-    for (uint32_t b = blockIdx.x; b < total; b += (C::MAP == 2 ? gridDim.x : total)) {
-        uint32_t s, c;
-        item_coords<C>(b, cps, nstripes, s, c);
-        bad |= encode_item<KT, M, CHECK, C>(pp, s, c, k, len, cps);
-    }
-    if constexpr (CHECK) {
-        if (bad)
-            atomicOr(flag, 1u);
-    }
-}
-
-// ------------------------------------------------------------ reconstruct
-
-// Per-stripe recovery plan; every value is uniform across the workgroup.
-struct RecPlan {
-    int x, y;          // lost data strips (x < y), -1 = none
-    int nd;            // number of lost data strips
-    bool lostP, lostQ; // parity strips to regenerate
-    bool needq;        // the Q syndrome over the survivors is needed
-    bool skip;         // unrecoverable / nothing to do
-    bool bad;          // more failures than M parities, or an index outside the stripe
-    uint32_t lost;     // bit j set: strip j is lost (decode_failures_mask only)
-    MulTable t1, t2;   // constant multipliers (see plan_constants)
-};
-
-// The stripe's two failure bytes, fail[2s] | fail[2s+1] << 8, through aligned word
-// reads at a wave-uniform address -- scalar loads.  A byte load would be a vector
-// memory instruction, and an item whose first instruction waits a full memory
-// round trip before the plan is known, and only then issues its strip loads,
-// takes half as long again.
-__device__ __forceinline__ uint32_t load_fail_pair(const uint8_t* fail, uint32_t s)
-{
-    const uintptr_t a = reinterpret_cast<uintptr_t>(fail) + 2 * static_cast<uintptr_t>(s);
-    // constant address space: the table is input only, never written by the kernel
-    typedef const uint32_t __attribute__((address_space(4)))* ccw;
-    const ccw w = (ccw)(a & ~static_cast<uintptr_t>(3));
-    const uint32_t at = static_cast<uint32_t>(a) & 3u;
-    uint32_t v = w[0] >> (at * 8u);
-    if (at == 3u)  // the pair straddles two words (a table at an odd address)
-        v |= w[1] << 8;
-    return v & 0xffffu;
-}
-
-// Decodes the (wave-uniform) failure pair: which strips are lost, which
-// syndromes are needed.  No table lookups -- runs before any load is issued, on
-// the scalar unit, so it is written without branches: every wave of every item
-// runs it ahead of its first strip load.
-template <int M>
-__device__ __forceinline__ RecPlan decode_failures(int k, uint32_t f0, uint32_t f1)
-{
-    RecPlan pl;
-    constexpr int kNone = 0x7fffffff;  // 0xff: no failure in this slot
-    const int ra = static_cast<int>(__builtin_amdgcn_readfirstlane(f0));
-    const int rb = static_cast<int>(__builtin_amdgcn_readfirstlane(f1));
-    const int a = ra == 0xff ? kNone : ra, b = rb == 0xff ? kNone : rb;
-    const bool da = a < k, db = b < k && b != a;  // lost data strips
-    pl.nd = (da ? 1 : 0) + (db ? 1 : 0);
-    const int lo = da ? a : (db ? b : -1);
-    const int hi = (da && db) ? b : -1;
-    pl.x = (hi >= 0 && hi < lo) ? hi : lo;
-    pl.y = (hi >= 0 && hi < lo) ? lo : hi;
-    pl.lostP = a == k || b == k;
-    pl.lostQ = a == k + 1 || b == k + 1;
-    const bool oob = (a != kNone && a >= k + M) || (b != kNone && b >= k + M);
-    if (M == 1)
-        pl.lostQ = false;  // index k + 1 is outside a RAID5 stripe (counted by oob)
-    const int nf = pl.nd + (pl.lostP ? 1 : 0) + (pl.lostQ ? 1 : 0);
-    pl.skip = (nf == 0) || (nf > M);
-    pl.bad = oob || nf > M;
-    pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
-    return pl;
-}
-
-// The same decode for a stripe of at most 32 strips known at compile time, over a
-// bit mask of the lost strips: a third of the scalar instructions, and "is strip
-// j lost" becomes a one-instruction bit test per load.  Every wave of a split
-// item runs this ahead of its strip loads, so its length is item latency.
-template <int K, int M>
-__device__ __forceinline__ RecPlan decode_failures_mask(uint32_t f0, uint32_t f1)
-{
-    static_assert(K + M <= 32, "one mask word");
-    constexpr uint32_t N = K + M, DATA = (K >= 32) ? 0xffffffffu : ((1u << K) - 1u);
-    RecPlan pl;
-    const uint32_t a = __builtin_amdgcn_readfirstlane(f0), b = __builtin_amdgcn_readfirstlane(f1);
-    const uint32_t L = (a < N ? 1u << a : 0u) | (b < N ? 1u << b : 0u);
-    const bool oob = (a >= N && a != 0xffu) || (b >= N && b != 0xffu);
-    const uint32_t D = L & DATA;
-    pl.lost = L;
-    pl.nd = __builtin_popcount(D);
-    pl.x = __builtin_ffs(static_cast<int>(D)) - 1;                  // lowest lost data strip, or -1
-    pl.y = pl.nd == 2 ? 31 - __builtin_clz(D) : -1;
-    pl.lostP = (L >> K) & 1u;
-    pl.lostQ = M == 2 && ((L >> (K + 1)) & 1u);
-    const int nf = __builtin_popcount(L);
-    pl.skip = (nf == 0) || (nf > M);
-    pl.bad = oob || nf > M;
-    pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
-    return pl;
-}
-
-// GF constants of the plan from exp/log tables (gf_vect_mul.c:255-268 for
-// 2^-x, :296-326 for the D+D constants A and B).
-__device__ __forceinline__ void plan_constants(RecPlan& pl, const uint8_t* t_exp,
-                                               const uint8_t* t_log)
-{
-    uint32_t c1 = 0, c2 = 0;
-    if (pl.nd == 1 && !pl.lostP && pl.lostQ) {
-        c1 = t_exp[pl.x];                                   // Q = Qs ^ 2^x D_x
-    } else if (pl.nd == 1 && pl.lostP) {
-        c1 = t_exp[255 - pl.x];                             // D_x = 2^-x (Q ^ Qs)
-    } else if (pl.nd == 2) {
-        const uint32_t gyx = t_exp[pl.y - pl.x];
-        const uint32_t den = t_exp[255 - t_log[gyx ^ 1u]];  // 1 / (2^(y-x) ^ 1)
-        c1 = t_exp[t_log[gyx] + t_log[den]];                // A = 2^(y-x) / (...)
-        c2 = t_exp[(255 - pl.x) + t_log[den]];              // B = 2^-x / (...)
-    }
-    // Wave-uniform (one stripe per workgroup): the table build runs on the SALU.
-    c1 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c1));
-    c2 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c2));
-    pl.t1 = make_mul_table(c1);
-    pl.t2 = make_mul_table(c2);
-}
-
-// Loads and syndrome accumulation for U elements, then `constants(pl)` (which
-// may stage tables and hit a workgroup barrier -- every lane calls it exactly
-// once, after its loads are in flight), then the outputs.
-// QS == false: the plan needs no Q syndrome (one data strip rebuilt from P, or P
-// alone regenerated), so the Horner doublings -- most of the kernel's VALU work --
-// are not compiled into this instance at all.
-template <int KT, int M, int U, int POL, bool BOUNDED, bool NOMUL, bool QS, class W, class Ptrs,
-          class F>
-__device__ __forceinline__ void recover_elems(const Ptrs& pp, uint32_t s, int k, RecPlan& pl,
-                                              uint32_t i0, uint32_t stride, uint32_t n,
-                                              F&& constants)
-{
-    using MW = Mem<W>;
-    const uint8_t* pP = pp.get(s, k);
-    const uint8_t* pQ = (M == 2) ? pp.get(s, k + 1) : pP;
-    // Lost (or unneeded) strips are skipped with wave-uniform branches: their
-    // pointers stay scalar, no load depends on another, and every surviving
-    // load of the lane is in flight before the first XOR.  (Re-pointing a lost
-    // strip at an address already loaded lets the compiler forward that value,
-    // which makes every later load wait for it.)
-    const bool useP = !pl.lostP;
-    const bool useQ = pl.needq && !pl.lostQ;
-    W ps[U], qs[U], pv[U], qv[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        ok[u] = !BOUNDED || i0 + u * stride < n;
-        ps[u] = W(0);
-        qs[u] = W(0);
-        pv[u] = (useP && ok[u]) ? MW::template ld<POL>(pP, i0 + u * stride) : W(0);
-        qv[u] = (useQ && ok[u]) ? MW::template ld<POL>(pQ, i0 + u * stride) : W(0);
-    }
-    auto fold = [&](const W(&d)[U]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            ps[u] ^= d[u];
-            if constexpr (M == 2 && QS)
-                qs[u] = gf_mul2(qs[u]) ^ d[u];
-        }
-    };
-    if constexpr (KT > 0) {
-        for_sources_desc<KT>(k, [&](int j) {
-            const bool live = (j != pl.x) && (j != pl.y);
-            W d[U];
-            const uint8_t* src = pp.get(s, j);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                d[u] = (live && ok[u]) ? MW::template ld<POL>(src, i0 + u * stride) : W(0);
-            fold(d);
-        });
-    } else {
-        const int x = pl.x, y = pl.y;
-        for_blocks_desc<U, POL, W>(
-            pp, s, k, ok, i0, stride, [=](int j) { return j != x && j != y; }, fold);
-    }
-    constants(pl);
-    const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
-    const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if (!ok[u])
-            continue;
-        const uint32_t i = i0 + u * stride;
-        if constexpr (M == 1) {
-            // RAID5: the one lost strip (data or P) is the XOR of the survivors
-            MW::template st<POL>(pl.nd == 0 ? pP : pX, i, pv[u] ^ ps[u]);
-        } else if (pl.nd == 0) {
-            if (pl.lostP)
-                MW::template st<POL>(pP, i, ps[u]);
-            if (M == 2 && pl.lostQ)
-                MW::template st<POL>(pQ, i, qs[u]);
-        } else if (pl.nd == 1) {
-            if (!pl.lostP) {
-                const W dx = pv[u] ^ ps[u];
-                MW::template st<POL>(pX, i, dx);
-                if (M == 2 && pl.lostQ)
-                    MW::template st<POL>(pQ, i, qs[u] ^ gf_mulc(pl.t1, dx));
-            } else {
-                const W dx = gf_mulc(pl.t1, qv[u] ^ qs[u]);
-                MW::template st<POL>(pX, i, dx);
-                MW::template st<POL>(pP, i, ps[u] ^ dx);
-            }
-        } else {
-            const W pxy = pv[u] ^ ps[u];
-            const W qxy = qv[u] ^ qs[u];
-            // NOMUL: diagnostic builds only (tools/sweep.py) -- wrong results.
-            const W dx = NOMUL ? (pxy ^ qxy) : (gf_mulc(pl.t1, pxy) ^ gf_mulc(pl.t2, qxy));
-            MW::template st<POL>(pX, i, dx);
-            MW::template st<POL>(pY, i, pxy ^ dx);
-        }
-    }
-}
-
-// Tables for the plan's constants, read with wave-uniform indices through scalar
-// loads (their own counter: they complete while the strip loads are in flight,
-// with no LDS staging and no barrier).
-//   lden[d]  log of 1 / (2^d ^ 1), 0 < d < 255 -- the one inverse of the D+D
-//            constants (gf_vect_mul.c:296-326), as a word image of a byte table
-//   mul[i]   the MulTable of the constant 2^i (5 words used of 8), i < 255
-// Every constant of a plan is a power of two (2^x, 2^-x, A = 2^(d + lden[d]),
-// B = 2^(255 - x + lden[d])), so its table is one 32-byte read by exponent
-// instead of ~55 scalar operations building it.
-struct PlanTables {
-    uint32_t lden[64];
-    uint32_t mul[255][8];
-};
-
-constexpr PlanTables make_plan_tables()
-{
-    const GfTables g = make_gf_tables();
-    PlanTables t{};
-    for (int d = 1; d < 255; ++d) {
-        const uint32_t l = (255u - g.log[g.exp[d] ^ 1u]) % 255u;
-        t.lden[d >> 2] |= l << ((d & 3) * 8);
-    }
-    for (int i = 0; i < 255; ++i) {
-        uint32_t p[8] = {};
-        for (int b = 0; b < 8; ++b)
-            p[b] = g.exp[i + b];  // 2^i * 2^b
-        // same layout as make_mul_table / tri_words
-        t.mul[i][0] = (p[0] << 8) | (p[1] << 16) | ((p[0] ^ p[1]) << 24);
-        t.mul[i][1] = t.mul[i][0] ^ (p[2] * 0x01010101u);
-        t.mul[i][2] = (p[3] << 8) | (p[4] << 16) | ((p[3] ^ p[4]) << 24);
-        t.mul[i][3] = t.mul[i][2] ^ (p[5] * 0x01010101u);
-        t.mul[i][4] = (p[6] << 8) | (p[7] << 16) | ((p[6] ^ p[7]) << 24);
-    }
-    return t;
-}
-
-__constant__ PlanTables c_plan = make_plan_tables();
-
-__device__ __forceinline__ uint32_t word_byte(const uint32_t* t, uint32_t idx)
-{
-    return (t[idx >> 2] >> ((idx & 3u) << 3)) & 0xffu;
-}
-
-// MulTable of 2^e, e < 510.
-__device__ __forceinline__ MulTable mul_table_exp2(uint32_t e)
-{
-    e = e >= 255u ? e - 255u : e;
-    const uint32_t* w = c_plan.mul[e];
-    MulTable t;
-    t.t0[0] = w[0];
-    t.t0[1] = w[1];
-    t.t1[0] = w[2];
-    t.t1[1] = w[3];
-    t.t2 = w[4];
-    return t;
-}
-
-// The plan's two multiplication tables from scalar reads of c_plan; the same
-// constants as plan_constants.
-struct PlanMul {
-    MulTable t1, t2;
-};
-__device__ __forceinline__ PlanMul plan_constants_scalar(int nd, int x, int y, bool lostP,
-                                                         bool lostQ)
-{
-    PlanMul m{};
-    if (nd == 1 && !lostP && lostQ) {
-        m.t1 = mul_table_exp2(x);                          // Q = Qs ^ 2^x D_x
-    } else if (nd == 1 && lostP) {
-        m.t1 = mul_table_exp2(255u - x);                   // D_x = 2^-x (Q ^ Qs)
-    } else if (nd == 2) {
-        const uint32_t d = static_cast<uint32_t>(y - x);
-        const uint32_t l = word_byte(c_plan.lden, d);
-        m.t1 = mul_table_exp2(d + l);                      // A = 2^(y-x) / (2^(y-x) ^ 1)
-        m.t2 = mul_table_exp2(255u - x + l);               // B = 2^-x / (2^(y-x) ^ 1)
-    }
-    return m;
-}
-
-// LDS image of the exp/log tables (768 B).
-struct LdsGf {
-    uint32_t w[(512 + 256) / 4];
-};
-
-template <int NTHR>
-__device__ __forceinline__ void stage_gf_tables(LdsGf& lds)
-{
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(&c_gf);
-    for (int t = threadIdx.x; t < (512 + 256) / 4; t += NTHR)
-        lds.w[t] = g[t];
-    __syncthreads();
-}
-
-// The GF tables staged through registers: each lane loads its words FIRST, before
-// any strip load (vmcnt retires in issue order, so the LDS write then waits only
-// for them, not for the strip loads issued after), and writes them to LDS once
-// its strip loads are in flight -- staging and barrier overlap the loads.
-template <int NTHR>
-struct TabStage {
-    static constexpr int kWords = (512 + 256) / 4;
-    static constexpr int kPerLane = (kWords + NTHR - 1) / NTHR;
-    uint32_t w[kPerLane];
-    __device__ __forceinline__ void load()
-    {
-#pragma unroll
-        for (int i = 0; i < kPerLane; ++i) {
-            const int t = threadIdx.x + i * NTHR;
-            w[i] = t < kWords ? reinterpret_cast<const uint32_t*>(&c_gf)[t] : 0u;
-        }
-    }
-    __device__ __forceinline__ void put(LdsGf& lds) const
-    {
-#pragma unroll
-        for (int i = 0; i < kPerLane; ++i) {
-            const int t = threadIdx.x + i * NTHR;
-            if (t < kWords)
-                lds.w[t] = w[i];
-        }
-    }
-    __device__ __forceinline__ void store(LdsGf& lds) const
-    {
-        put(lds);
-        __syncthreads();
-    }
-};
-
-template <int KT, int M, class C, class Ptrs, class F>
-__device__ __forceinline__ void reconstruct_item(const Ptrs& pp, uint32_t s, uint32_t c, int k,
-                                                 uint32_t len, uint32_t cps, RecPlan& pl,
-                                                 F&& constants)
-{
-    constexpr int NTHR = C::NTHR, U = C::U, POL = C::POL;
-    constexpr uint32_t EPB = static_cast<uint32_t>(NTHR) * U;
-    const uint32_t nvec = len >> 4;
-    auto none = [](RecPlan&) {};
-    if (stripe_aligned<KT, M>(pp, s, k)) {
-        const uint32_t i0 = c * EPB + threadIdx.x;
-        if ((c + 1) * EPB <= nvec) {
-            if (M == 2 && !pl.needq)  // wave-uniform
-                recover_elems<KT, M, U, POL, false, C::PLAN == 3, false, u32x4>(
-                    pp, s, k, pl, i0, NTHR, nvec, constants);
-            else
-                recover_elems<KT, M, U, POL, false, C::PLAN == 3, true, u32x4>(
-                    pp, s, k, pl, i0, NTHR, nvec, constants);
-        } else {
-            // Partial last chunk (rare): one vector at a time keeps this path's
-            // registers below the main path's, so it does not cap occupancy.
-            constants(pl);
-#pragma unroll 1
-            for (int u = 0; u < U; ++u)
-                recover_elems<KT, M, 1, POL, true, false, true, u32x4>(pp, s, k, pl, i0 + u * NTHR, NTHR, nvec,
-                                                          none);
-        }
-        const uint32_t tail = len & 15u;
-        if (tail && c == cps - 1 && threadIdx.x < tail)
-            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, k, pl, nvec * 16 + threadIdx.x,
-                                                      NTHR, len, none);
-    } else {
-        constants(pl);
-        const uint32_t b1 = min(len, (c + 1) * EPB * 16);
-        for (uint32_t b = c * EPB * 16 + threadIdx.x; b < b1; b += NTHR)
-            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, k, pl, b, NTHR, b1, none);
-    }
-}
-
-template <int KT, int M, class C, class Ptrs>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(Ptrs pp, uint32_t k_rt, uint32_t len,
-                                                         uint32_t cps, uint32_t nstripes,
-                                                         const uint8_t* fail, uint32_t f01,
-                                                         uint32_t* bad)
-{
-    __shared__ LdsGf lds;
-    const uint8_t* l_exp = reinterpret_cast<const uint8_t*>(lds.w);
-    const uint8_t* l_log = l_exp + 512;
-    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
-    const uint32_t total = cps * nstripes;
-    if constexpr (C::MAP == 2)
-        stage_gf_tables<C::NTHR>(lds);  // once per persistent workgroup
-    TabStage<C::NTHR> tabs;
-    if constexpr (M == 2 && C::MAP != 2 && C::PLAN == 0)
-        tabs.load();
-    for (uint32_t b = blockIdx.x; b < total; b += (C::MAP == 2 ? gridDim.x : total)) {
-        uint32_t s, c;
-        item_coords<C>(b, cps, nstripes, s, c);
-        uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
-        if (fail) {
-            // The pair is read with byte (vector) loads for the P+Q widths 8..12 and
-            // through scalar word loads otherwise: measured, not derived -- same-box
-            // A/B of whole library builds (tools/gpu_lib_ab_shapes.sh, profiles/r02/
-            // split/fail_read_ab.jsonl), microseconds per launch, vector vs scalar:
-            // 8+2 x 64 KiB dual 409.8 vs 417.6, 10+2 497 vs 506, 12+2 301 vs 305; but
-            // 5+2 305 vs 288, 4+1 213 vs 203, 3+1 353 vs 328, 8+2 x 128 KiB single 385 vs
-            // 380, 14+2 347 vs 343.
-            if constexpr (M == 2 && KT >= 8 && KT <= 12) {
-                f0 = fail[2 * (size_t)s];
-                f1 = fail[2 * (size_t)s + 1];
-            } else {
-                const uint32_t f = load_fail_pair(fail, s);
-                f0 = f & 0xffu;
-                f1 = f >> 8;
-            }
-        }
-        RecPlan pl = decode_failures<M>(k, f0, f1);
-        // A stripe that cannot be rebuilt is left untouched and counted once (by
-        // the workgroup of its first chunk) when the caller asked for the count.
-        // Skipped stripes are the only ones counted before any load: a store or
-        // atomic ahead of the pointer-table reads would keep them from being
-        // scalar loads.
-        const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
-        if (pl.skip) {
-            if (count_bad)
-                atomicAdd(bad, 1u);
-            continue;  // uniform across the workgroup
-        }
-        if constexpr (M == 1) {
-            // RAID5 rebuilds by XOR alone: no constants, no tables, no barrier
-            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [](RecPlan&) {});
-        } else if constexpr (C::PLAN == 2 || C::PLAN == 3) {
-            // DIAGNOSTIC ONLY (tools/sweep.py): constants left zero, no LDS, no
-            // barrier -- wrong results, measures what the plan step costs.
-            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-                p.t1 = make_mul_table(0);
-                p.t2 = make_mul_table(0);
-            });
-        } else if constexpr (C::PLAN == 4) {
-            // constants from scalar reads of c_plan: no LDS, no barrier
-            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-                const PlanMul mul = plan_constants_scalar(p.nd, p.x, p.y, p.lostP, p.lostQ);
-                p.t1 = mul.t1;
-                p.t2 = mul.t2;
-            });
-        } else if constexpr (C::PLAN == 1) {
-            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-                plan_constants(p, c_gf.exp, c_gf.log);
-            });
-        } else if constexpr (C::MAP == 2) {
-            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-                plan_constants(p, l_exp, l_log);
-            });
-        } else {
-            // Stage the tables while this lane's strip loads are in flight.
-            reconstruct_item<KT, M, C>(pp, s, c, k, len, cps, pl, [&](RecPlan& p) {
-                tabs.store(lds);
-                plan_constants(p, l_exp, l_log);
-            });
-        }
-        if (count_bad)
-            atomicAdd(bad, 1u);
-    }
-}
-
-// ------------------------------------------------------------ split items
-//
-// The same item (1 KiB of every strip of one stripe) shared by SPLIT waves of one
-// workgroup.  A wave that loads all k strips of an item keeps k KiB in flight and
-// holds its slot until the last of them has arrived; the CU then either has few
-// waves (idle slots while workgroups turn over) or far more bytes in flight than
-// the memory system needs, and DRAM efficiency falls as k grows (16+2: 6.0 TB/s).
-// With the strips of the item dealt over 3-4 waves every wave has 2-4 loads, a CU
-// holds 6 items instead of 16-24, and the same shapes stream 5-7% faster
-// (tools/probe/wide_probe.hip: 8+2 x 64 KiB 6.96 vs 6.64 TB/s, 16+2 x 256 KiB
-// 6.42 vs 6.00).  Wave w accumulates P and the Horner form of Q over its strips
-// [w*KW, (w+1)*KW), scales its Q part by 2^(w*KW), and the parts are XORed
-// through LDS after one barrier.
-
-// Split kernels take a 2-D/3-D grid -- x the chunk, y (and z beyond 65535) the
-// stripe -- so an item's coordinates cost no division.  A grid whose x extent is
-// tiny dispatches slowly (8+2 x 4 KiB strips, x = 4: 531 us per launch against 444
-// for the same items on a 1-D grid), so when a strip has fewer than 64 chunks and
-// their number is a power of two, 2^fold neighbouring stripes share one x row:
-// x = chunk | stripe_low << cshift.  Otherwise fold = 0 and cshift = 31 (x < 2^31,
-// so the same two shifts and the mask leave chunk = x, stripe_low = 0).
-constexpr uint32_t kGridY = 65535;
-struct ItemGrid {
-    uint32_t cshift, fold;
-    __device__ __forceinline__ void coords(uint32_t& c, uint32_t& s) const
-    {
-        c = blockIdx.x & ((1u << cshift) - 1u);
-        s = ((blockIdx.z * kGridY + blockIdx.y) << fold) + (blockIdx.x >> cshift);
-    }
-};
-
-template <int SPLIT>
-struct SplitLds {
-    u32x4 p[SPLIT][64];
-    u32x4 q[SPLIT][64];
-};
-
-// 2^e in GF(2^8); e is a compile-time constant wherever this is used, so the
-// multiplication table built from it folds into immediates.
-__host__ __device__ constexpr uint32_t gf_exp2_const(int e)
-{
-    uint32_t c = 1;
-    for (int i = 0; i < e; ++i)
-        c = ((c << 1) ^ ((c & 0x80u) ? 0x1du : 0u)) & 0xffu;
-    return c;
-}
-
-// Partial sums of one wave.
-struct PartPQ {
-    u32x4 p, q;
-};
-
-// Returns part(std::integral_constant<int, W>) for the wave's own index W = w
-// (wave-uniform, scalar branches).  Each wave gets code specialised for its
-// strips: strip indices are constants, so a pointer table row is fetched with
-// scalar loads of fixed offsets (a run-time strip index turns them into per-lane
-// loads plus a readfirstlane loop around every strip access).  The parts come
-// back by value -- sums captured by reference end up in scratch memory.
-template <int W, int SPLIT, class F>
-__device__ __forceinline__ auto wave_case(uint32_t w, const F& part)
-{
-    if constexpr (W + 1 == SPLIT) {
-        return part(std::integral_constant<int, W>{});
-    } else {
-        if (w == W)
-            return part(std::integral_constant<int, W>{});
-        return wave_case<W + 1, SPLIT>(w, part);
-    }
-}
-
-template <int SPLIT>
-__device__ __forceinline__ u32x4 split_sum(const u32x4 (&part)[SPLIT][64], uint32_t lane)
-{
-    u32x4 a = part[0][lane];
-#pragma unroll
-    for (int t = 1; t < SPLIT; ++t)
-        a ^= part[t][lane];
-    return a;
-}
-
-// Vector i of every strip: wave 0 ends up storing (or checking) P, the last wave Q.
-template <int KT, int M, int SPLIT, int POL, bool CHECK, bool BOUNDED, class Ptrs>
-__device__ __forceinline__ bool encode_split_vec(const Ptrs& pp, uint32_t s, uint32_t w,
-                                                 uint32_t lane, uint32_t i, uint32_t nvec,
-                                                 SplitLds<SPLIT>& lds)
-{
-    using MW = Mem<u32x4>;
-    constexpr int KW = (KT + SPLIT - 1) / SPLIT;
-    const bool ok = !BOUNDED || i < nvec;
-    // Every pointer is fetched before the barrier: a table read after it can no
-    // longer be a scalar load (LDS writes and the barrier count as clobbers).
-    const uint8_t* dp = pp.get(s, KT);
-    const uint8_t* dq = (M == 2) ? pp.get(s, KT + 1) : dp;
-    const PartPQ part = wave_case<0, SPLIT>(w, [=, &pp](auto wc) __attribute__((always_inline)) {
-        constexpr int J0 = decltype(wc)::value * KW;
-        u32x4 p = 0, q = 0;
-#pragma unroll
-        for (int j = KW - 1; j >= 0; --j) {
-            u32x4 d = 0;
-            if (J0 + j < KT && ok)
-                d = MW::template ld<POL>(pp.get(s, J0 + j), i);
-            p ^= d;
-            if constexpr (M == 2)
-                q = gf_mul2(q) ^ d;
-        }
-        if constexpr (M == 2 && J0 != 0)
-            q = gf_mulc(make_mul_table(gf_exp2_const(J0)), q);
-        return PartPQ{p, q};
-    });
-    lds.p[w][lane] = part.p;
-    if constexpr (M == 2)
-        lds.q[w][lane] = part.q;
-    __syncthreads();
-    bool bad = false;
-    if (w == 0) {
-        const u32x4 a = split_sum<SPLIT>(lds.p, lane);
-        if (ok) {
-            if constexpr (CHECK)
-                bad = MW::any(MW::template ld<0>(dp, i) ^ a);
-            else
-                MW::template st<POL>(dp, i, a);
-        }
-    }
-    if constexpr (M == 2) {
-        if (w == SPLIT - 1) {
-            const u32x4 a = split_sum<SPLIT>(lds.q, lane);
-            if (ok) {
-                if constexpr (CHECK)
-                    bad = MW::any(MW::template ld<0>(dq, i) ^ a);
-                else
-                    MW::template st<POL>(dq, i, a);
-            }
-        }
-    }
-    return bad;
-}
-
-// The 16-byte vectors go through the split path; a byte tail (len % 16) and
-// strips that are not 16-byte aligned take the one-wave byte path on wave 0.
-template <int KT, int M, bool CHECK, class C, class Ptrs>
-__device__ __forceinline__ bool encode_item_split(const Ptrs& pp, uint32_t s, uint32_t c,
-                                                  uint32_t len, uint32_t cps,
-                                                  SplitLds<C::SPLIT>& lds)
-{
-    constexpr int SPLIT = C::SPLIT, POL = C::POL;
-    constexpr uint32_t L = 64;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t nvec = len >> 4;
-    bool bad = false;
-    if (stripe_aligned<KT, M>(pp, s, KT)) {
-        const uint32_t i = c * L + lane;
-        if ((c + 1) * L <= nvec)
-            bad = encode_split_vec<KT, M, SPLIT, POL, CHECK, false>(pp, s, w, lane, i, nvec, lds);
-        else
-            bad = encode_split_vec<KT, M, SPLIT, POL, CHECK, true>(pp, s, w, lane, i, nvec, lds);
-        const uint32_t tail = len & 15u;
-        if (w == 0 && tail && c == cps - 1 && lane < tail)
-            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(pp, s, KT, nvec * 16 + lane, L,
-                                                                    len);
-    } else if (w == 0) {
-        const uint32_t b1 = min(len, (c + 1) * L * 16);
-        for (uint32_t b = c * L * 16 + lane; b < b1; b += L)
-            bad |= encode_elems<0, M, 1, 0, CHECK, true, uint32_t>(pp, s, KT, b, L, b1);
-    }
-    return bad;
-}
-
-template <int KT, int M, bool CHECK, class C, class Ptrs>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_split(
-    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, uint32_t* flag, ItemGrid ig)
-{
-    static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one split item per workgroup, stripe order");
-    __shared__ SplitLds<C::SPLIT> lds;
-    uint32_t c, s;
-    ig.coords(c, s);
-    if (s >= nstripes)
-        return;  // uniform: the ragged last z-slice
-    const bool bad = encode_item_split<KT, M, CHECK, C>(pp, s, c, len, cps, lds);
-    if constexpr (CHECK) {
-        if (bad)
-            atomicOr(flag, 1u);
-    }
-}
-
-// ---- shared reconstruct: loads dealt by strip, arithmetic dealt by column
-//
-// Dealing the reconstruct's ARITHMETIC by strip as the encode does (a Horner chain
-// per wave over its strips on whole 16-byte vectors, the Q part scaled by a
-// constant to line up, parts XORed through LDS) was built and measured: the
-// scaling costs 36 VALU per wave, which a VALU-heavy dual-failure rebuild cannot
-// afford (8+2: 580 VALU per item against 435 for one wave), and it lost to the
-// one-wave kernel below k = 16 (profiles/r02/split/).  Here only the LOADS are
-// dealt by strip: each wave loads its strips as 16-byte vectors and parks them in
-// LDS untouched (one row per strip; a strip that is lost or not needed arrives as
-// zeros through a descriptor with no records).  The surviving P rides on the last
-// wave and the surviving Q on the wave with the fewest data strips.  The plan's
-// constants come from scalar table reads placed between the issue of the strip
-// loads and the barrier.  After the one barrier every wave owns its share of the
-// item's 256 dword columns and runs the one Horner chain down all k strips of its
-// columns: the same arithmetic as the one-wave kernel, no scaling, spread evenly
-// over the waves whatever the failure pattern.
-template <int KT>
-struct ColLds {
-    u32x4 row[KT + 2][64];  // rows 0..KT-1 data strips, KT the surviving P, KT+1 the surviving Q
-};
-
-template <int KT, int M, int SPLIT, int POL, bool BOUNDED, bool QS, class Ptrs>
-__device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, RecPlan& pl,
-                                                 uint32_t w, uint32_t lane, uint32_t i,
-                                                 uint32_t nvec, ColLds<KT>& lds)
-{
-    using MW = Mem<u32x4>;
-    static_assert(SPLIT == 2 || SPLIT == 4, "every wave finishes 16 / SPLIT bytes per lane");
-    constexpr int KW = (KT + SPLIT - 1) / SPLIT;
-    constexpr int REM = SPLIT * KW - KT;
-    constexpr uint32_t WP = SPLIT - 1, WQ = REM >= 2 ? SPLIT - 1 : SPLIT - 2;
-    const bool ok = !BOUNDED || i < nvec;
-    const uint8_t* pP = pp.get(s, KT);
-    const uint8_t* pQ = (M == 2) ? pp.get(s, KT + 1) : pP;
-    const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
-    const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
-    const uint32_t lost = pl.lost;
-    const bool haveP = !pl.lostP, haveQ = M == 2 && QS && pl.needq && !pl.lostQ;
-    // phase 1: this wave's strips -> LDS rows (zeros for the ones it skips)
-    wave_case<0, SPLIT>(w, [=, &pp, &lds](auto wc) __attribute__((always_inline)) {
-        constexpr uint32_t W = decltype(wc)::value;
-        constexpr int J0 = static_cast<int>(W) * KW;
-        u32x4 d[KW], pv = 0, qv = 0;
-#pragma unroll
-        for (int j = KW - 1; j >= 0; --j) {
-            d[j] = 0;
-            if (J0 + j < KT)
-                d[j] = ok ? MW::template ld_if<POL>(pp.get(s, J0 + j), i, !((lost >> (J0 + j)) & 1u))
-                          : u32x4(0);
-        }
-        if constexpr (W == WP)
-            pv = ok ? MW::template ld_if<POL>(pP, i, haveP) : u32x4(0);
-        if constexpr (W == WQ)
-            qv = ok ? MW::template ld_if<POL>(pQ, i, haveQ) : u32x4(0);
-#pragma unroll
-        for (int j = KW - 1; j >= 0; --j)
-            if (J0 + j < KT)
-                lds.row[J0 + j][lane] = d[j];
-        if constexpr (W == WP)
-            lds.row[KT][lane] = pv;
-        if constexpr (W == WQ)
-            lds.row[KT + 1][lane] = qv;
-        return PartPQ{};
-    });
-    if constexpr (M == 2) {
-        const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
-        pl.t1 = mul.t1;
-        pl.t2 = mul.t2;
-    }
-    __syncthreads();
-    // phase 2: this wave's columns, all strips
-    constexpr int ND = 4 / SPLIT;
-    const uint32_t t = (w * 64u + lane) * ND;
-    const uint32_t ob = ((i - lane) << 4) + t * 4u;
-    const bool okw = !BOUNDED || ob < (nvec << 4);
-    const uint32_t* L = reinterpret_cast<const uint32_t*>(lds.row);
-    uint32_t pt[ND], qt[ND];
-#pragma unroll
-    for (int n = 0; n < ND; ++n) {
-        pt[n] = 0;
-        qt[n] = 0;
-    }
-#pragma unroll
-    for (int j = KT - 1; j >= 0; --j) {
-#pragma unroll
-        for (int n = 0; n < ND; ++n) {
-            const uint32_t d = L[j * 256 + t + n];
-            pt[n] ^= d;
-            if constexpr (M == 2 && QS)
-                qt[n] = gf_mul2(qt[n]) ^ d;
-        }
-    }
-#pragma unroll
-    for (int n = 0; n < ND; ++n) {
-        pt[n] ^= L[KT * 256 + t + n];
-        if constexpr (M == 2 && QS)
-            qt[n] ^= L[(KT + 1) * 256 + t + n];
-    }
-    if (!okw)
-        return;
-    uint32_t o1[ND], o2[ND];
-    if constexpr (M == 1) {
-        st_words<POL, ND>(pl.nd == 0 ? pP : pX, ob, pt);  // RAID5: XOR of the survivors
-    } else if (pl.nd == 0) {
-        if (pl.lostP)
-            st_words<POL, ND>(pP, ob, pt);
-        if (M == 2 && pl.lostQ)
-            st_words<POL, ND>(pQ, ob, qt);
-    } else if (pl.nd == 1) {
-        if (!pl.lostP) {
-            st_words<POL, ND>(pX, ob, pt);
-            if (M == 2 && pl.lostQ) {
-#pragma unroll
-                for (int n = 0; n < ND; ++n)
-                    o2[n] = qt[n] ^ gf_mulc(pl.t1, pt[n]);
-                st_words<POL, ND>(pQ, ob, o2);
-            }
-        } else {
-#pragma unroll
-            for (int n = 0; n < ND; ++n) {
-                o1[n] = gf_mulc(pl.t1, qt[n]);
-                o2[n] = pt[n] ^ o1[n];
-            }
-            st_words<POL, ND>(pX, ob, o1);
-            st_words<POL, ND>(pP, ob, o2);
-        }
-    } else {
-#pragma unroll
-        for (int n = 0; n < ND; ++n) {
-            o1[n] = gf_mulc(pl.t1, pt[n]) ^ gf_mulc(pl.t2, qt[n]);
-            o2[n] = pt[n] ^ o1[n];
-        }
-        st_words<POL, ND>(pX, ob, o1);
-        st_words<POL, ND>(pY, ob, o2);
-    }
-}
-
-template <int KT, int M, class C, class Ptrs>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_cols(
-    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, const uint8_t* fail, uint32_t f01,
-    uint32_t* bad, ItemGrid ig)
-{
-    static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one shared item per workgroup, stripe order");
-    constexpr int SPLIT = C::SPLIT, POL = C::POL;
-    __shared__ ColLds<KT> lds;
-    uint32_t c, s;
-    ig.coords(c, s);
-    if (s >= nstripes)
-        return;
-    const bool aligned = stripe_aligned<KT, M>(pp, s, KT);
-    uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
-    if (fail) {
-        const uint32_t f = load_fail_pair(fail, s);
-        f0 = f & 0xffu;
-        f1 = f >> 8;
-    }
-    RecPlan pl = decode_failures_mask<KT, M>(f0, f1);
-    const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
-    if (!pl.skip) {
-        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-        const uint32_t nvec = len >> 4;
-        auto none = [](RecPlan&) {};
-        if (aligned) {
-            const uint32_t i = c * 64u + lane;
-            if ((c + 1) * 64u <= nvec) {
-                if (M == 2 && !pl.needq)
-                    recover_cols_vec<KT, M, SPLIT, POL, false, false>(pp, s, pl, w, lane, i, nvec, lds);
-                else
-                    recover_cols_vec<KT, M, SPLIT, POL, false, true>(pp, s, pl, w, lane, i, nvec, lds);
-            } else {
-                recover_cols_vec<KT, M, SPLIT, POL, true, true>(pp, s, pl, w, lane, i, nvec, lds);
-            }
-            const uint32_t tail = len & 15u;
-            if (w == 0 && tail && c == cps - 1 && lane < tail)
-                recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl,
-                                                                       nvec * 16 + lane, 64, len, none);
-        } else if (w == 0) {
-            const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
-            pl.t1 = mul.t1;
-            pl.t2 = mul.t2;
-            const uint32_t b1 = min(len, (c + 1) * 1024u);
-            for (uint32_t b = c * 1024u + lane; b < b1; b += 64)
-                recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, b, 64, b1, none);
-        }
-    }
-    if (count_bad)
-        atomicAdd(bad, 1u);
-}
-
-// ------------------------------------------------------------ segment work lists
-
-// Scatter-gather form (ec_ctx.cpp): a batch of variable-length segments, each
-// one contiguous run across the k+m strips of a stripe (what raid5_xor_stripe,
-// raid5_simple.c:141-203, hands to one xor_gen call).  The host expands the
-// segments into work items (segment, chunk) so one launch covers them all.
-struct WorkItem {
-    uint32_t seg;
-    uint32_t chunk;
-};
-
-// Where work item b comes from: an explicit (segment, chunk) list, or -- when
-// every queued segment has the same length (full-strip runs, fixed-size iovecs)
-// -- arithmetic, so the item costs no descriptor load at all.
-struct WorkSrc {
-    const WorkItem* list;      // nullptr: uniform segments
-    const uint32_t* seg_len;   // list mode
-    uint32_t ulen, ucps;       // uniform mode: segment length, items per segment
-    __device__ __forceinline__ void get(uint32_t b, uint32_t cb, uint32_t& seg, uint32_t& chunk,
-                                        uint32_t& len, uint32_t& cps) const
-    {
-        if (list) {
-            const WorkItem w = list[b];
-            seg = w.seg;
-            chunk = w.chunk;
-            len = seg_len[seg];
-            cps = (len + cb - 1) / cb;
-        } else {
-            seg = b / ucps;
-            chunk = b - seg * ucps;
-            len = ulen;
-            cps = ucps;
-        }
-    }
-};
-
-// Pointer-table reads of the one-wave work-list encode: ordinary reads for a
-// compiled width (the compiler makes them scalar loads, measured 2% faster than
-// constant-space reads there), constant-space reads for a run-time width, whose
-// strip index is a loop variable.
-template <int KT>
-using WorkEncPtrs = std::conditional_t<(KT > 0), TablePlain, TablePtrs>;
-
-template <int KT, int M, bool CHECK, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(
-    WorkEncPtrs<KT> pp, uint32_t k_rt, WorkSrc ws, uint32_t nwork)
-{
-    constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
-    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
-    for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
-        uint32_t seg, chunk, len, cps;
-        ws.get(b, CB, seg, chunk, len, cps);
-        encode_item<KT, M, CHECK, C>(pp, seg, chunk, k, len, cps);
-    }
-}
-
-// The shared-item encode over a segment list: one workgroup per work item.
-template <int KT, int M, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work_split(
-    TablePtrs pp, WorkSrc ws, uint32_t nwork)
-{
-    static_assert(KT > 0 && C::SPLIT > 1, "shared items need a compile-time width");
-    constexpr uint32_t CB = static_cast<uint32_t>(C::ITEM) * C::U * 16;
-    __shared__ SplitLds<C::SPLIT> lds;
-    uint32_t seg, chunk, len, cps;
-    ws.get(blockIdx.x, CB, seg, chunk, len, cps);
-    encode_item_split<KT, M, false, C>(pp, seg, chunk, len, cps, lds);
-}
-
-template <int KT, int M, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
-                                                              WorkSrc ws, const uint8_t* fail,
-                                                              uint32_t fstride, uint32_t nwork)
-{
-    __shared__ LdsGf lds;
-    const uint8_t* l_exp = reinterpret_cast<const uint8_t*>(lds.w);
-    const uint8_t* l_log = l_exp + 512;
-    constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
-    const int k = KT > 0 ? KT : static_cast<int>(k_rt);
-    TabStage<C::NTHR> tabs;
-    if constexpr (M == 2)
-        tabs.load();
-    for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x) {
-        uint32_t seg, chunk, len, cps;
-        ws.get(b, CB, seg, chunk, len, cps);
-        const uint8_t* f = fail + static_cast<size_t>(fstride) * seg;
-        RecPlan pl = decode_failures<M>(k, f[0], f[1]);
-        if (pl.skip)
-            continue;
-        if constexpr (M == 1) {
-            reconstruct_item<KT, M, C>(pp, seg, chunk, k, len, cps, pl, [](RecPlan&) {});
-        } else {
-            reconstruct_item<KT, M, C>(pp, seg, chunk, k, len, cps, pl, [&](RecPlan& p) {
-                tabs.store(lds);
-                plan_constants(p, l_exp, l_log);
-            });
-        }
-    }
-}
-
-// ------------------------------------------------------------ read-modify-write
-
-// Small-write parity update (raid5_stripe_write_preread_complete_rmw,
-// raid5.c:705-741, extended to Q): for the nd data chunks a segment touches,
-// with old contents O_i and new contents N_i at data index e_i,
-//   P' = P ^ XOR_i (O_i ^ N_i),   Q' = Q ^ XOR_i 2^{e_i} (O_i ^ N_i).
-// Each 2^{e_i} is a constant multiplication through the ready-made table of that
-// power (c_plan.mul, a scalar read): 9 VALU operations per dword whatever the
-// exponent, against up to k-1 doublings of 6.
-// Segment table row: [O_0, N_0, O_1, N_1, ..., P, (Q)]; exps row: e_0, e_1, ...
-// The row and the exponents are read through the constant address space, so the
-// strip bases stay in SGPRs (a base in VGPRs costs a readfirstlane loop around
-// every buffer access).  NDT = 1, 2: nd at compile time, every load of the item
-// issued before the first use; NDT = 0: run-time nd.
-
-// Byte idx of a device byte array that the kernel never writes: a scalar load of
-// the aligned word around it.
-__device__ __forceinline__ uint32_t load_const_byte(const uint8_t* a, size_t idx)
-{
-    const uintptr_t p = reinterpret_cast<uintptr_t>(a) + idx;
-    typedef const uint32_t __attribute__((address_space(4)))* ccw;
-    const uint32_t w = ((ccw)(p & ~static_cast<uintptr_t>(3)))[0];
-    return (w >> ((static_cast<uint32_t>(p) & 3u) * 8u)) & 0xffu;
-}
-
-template <int M, int NDT, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_update_work(
-    const uint8_t* const* tab, uint32_t nd_rt, const uint8_t* exps, WorkSrc ws, uint32_t nwork)
-{
-    constexpr uint32_t EPB = static_cast<uint32_t>(C::NTHR) * C::U;
-    static_assert(C::U == 1, "one vector per lane");
-    const uint32_t nd = NDT > 0 ? NDT : nd_rt;
-    const uint32_t b = blockIdx.x;  // one work item per workgroup
-    if (b >= nwork)
-        return;
-    uint32_t seg, chunk, len, cps;
-    ws.get(b, EPB * 16, seg, chunk, len, cps);
-    const TablePtrs row{tab, 2 * nd + M};
-    const uint8_t* pP = row.get(seg, static_cast<int>(2 * nd));
-    const uint8_t* pQ = M == 2 ? row.get(seg, static_cast<int>(2 * nd + 1)) : pP;
-    uintptr_t acc = reinterpret_cast<uintptr_t>(pP) | reinterpret_cast<uintptr_t>(pQ);
-    if constexpr (NDT > 0) {
-#pragma unroll
-        for (int t = 0; t < 2 * NDT; ++t)
-            acc |= reinterpret_cast<uintptr_t>(row.get(seg, t));
-    } else {
-        for (uint32_t t = 0; t < 2 * nd; ++t)
-            acc |= reinterpret_cast<uintptr_t>(row.get(seg, static_cast<int>(t)));
-    }
-    const size_t e0 = static_cast<size_t>(seg) * nd;
-    auto body = [&](auto tag, uint32_t i) __attribute__((always_inline)) {
-        using W = decltype(tag);
-        using MW = Mem<W>;
-        W dp = W(0), dq = W(0);
-        if constexpr (NDT > 0) {
-            W o[NDT], n[NDT];
-#pragma unroll
-            for (int t = 0; t < NDT; ++t) {
-                o[t] = MW::template ld<C::POL>(row.get(seg, 2 * t), i);
-                n[t] = MW::template ld<C::POL>(row.get(seg, 2 * t + 1), i);
-            }
-            const W p0 = MW::template ld<C::POL>(pP, i);
-            const W q0 = M == 2 ? MW::template ld<C::POL>(pQ, i) : W(0);
-#pragma unroll
-            for (int t = 0; t < NDT; ++t) {
-                const W delta = o[t] ^ n[t];
-                dp ^= delta;
-                if constexpr (M == 2)
-                    dq ^= gf_mulc(mul_table_exp2(load_const_byte(exps, e0 + t)), delta);
-            }
-            MW::template st<C::POL>(pP, i, p0 ^ dp);
-            if constexpr (M == 2)
-                MW::template st<C::POL>(pQ, i, q0 ^ dq);
-        } else {
-            const W p0 = MW::template ld<C::POL>(pP, i);
-            const W q0 = M == 2 ? MW::template ld<C::POL>(pQ, i) : W(0);
-            for (uint32_t t = 0; t < nd; ++t) {
-                const W delta = MW::template ld<C::POL>(row.get(seg, static_cast<int>(2 * t)), i) ^
-                                MW::template ld<C::POL>(row.get(seg, static_cast<int>(2 * t + 1)), i);
-                dp ^= delta;
-                if constexpr (M == 2)
-                    dq ^= gf_mulc(mul_table_exp2(load_const_byte(exps, e0 + t)), delta);
-            }
-            MW::template st<C::POL>(pP, i, p0 ^ dp);
-            if constexpr (M == 2)
-                MW::template st<C::POL>(pQ, i, q0 ^ dq);
-        }
-    };
-    if ((acc & 15u) == 0) {
-        const uint32_t nvec = len >> 4;
-        const uint32_t i = chunk * EPB + threadIdx.x;
-        if (i < nvec)
-            body(u32x4{}, i);
-        const uint32_t tail = len & 15u;
-        if (tail && chunk == cps - 1 && threadIdx.x < tail)
-            body(uint32_t{}, nvec * 16 + threadIdx.x);
-    } else {
-        const uint32_t b1 = min(len, (chunk + 1) * EPB * 16);
-        for (uint32_t i = chunk * EPB * 16 + threadIdx.x; i < b1; i += C::NTHR)
-            body(uint32_t{}, i);
-    }
-}
-
-// ------------------------------------------------------------ gf_vect_mul
-
-// dst = c * src through the caller's table (gf_vect_mul.c:108 call shape).  T is the
-// table form: the caller's two 16-entry nibble tables as they are (NibTable, 22
-// VALU operations per dword), or -- when the host found the table to be a linear
-// map, as every table from gf_vect_mul_init is -- the same map as three 3-bit
-// tables (MulTable, 9 operations).  One workgroup per NTHR * U vectors, no
-// grid-stride loop; POL as in the encode.  Measured through the synchronous call
-// on 1 GiB / 256 MiB (GB/s of read + write, tools/gpu_gfv_ab.sh, profiles/r02/
-// gf_vect_mul_ab.jsonl): one wave x one vector 6.51 / 5.89, 256 lanes x 1 6.41 /
-// 5.73, 256 x 2 5.97 / 5.51, 256 x 4 5.82 / 5.25, 64 x 4 6.14 / 5.47; global nt
-// instead of buffer accesses 6.32, plain 6.04.  The grid-stride kernel with the
-// nibble tables and plain accesses that this replaces: 4.48 / 4.80.
-#ifndef DRAID_GFV_NTHR
-#define DRAID_GFV_NTHR 64
-#endif
-#ifndef DRAID_GFV_U
-#define DRAID_GFV_U 1
-#endif
-#ifndef DRAID_GFV_POL
-#define DRAID_GFV_POL pol_aux(2, 18)
-#endif
-template <class T, int NTHR, int U, int POL>
-__global__ __launch_bounds__(NTHR) void k_gf_vect_mul(const uint8_t* src, uint8_t* dst,
-                                                      uint32_t len, T t)
-{
-    constexpr uint32_t VPB = static_cast<uint32_t>(NTHR) * U;  // vectors per workgroup
-    const uint32_t tid = threadIdx.x;
-    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
-        const uint32_t nvec = len >> 4;
-        const uint32_t i0 = blockIdx.x * VPB + tid;
-        u32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            v[u] = i0 + u * NTHR < nvec ? Mem<u32x4>::ld<POL>(src, i0 + u * NTHR) : u32x4(0);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (i0 + u * NTHR < nvec)
-                Mem<u32x4>::st<POL>(dst, i0 + u * NTHR, gf_mulc(t, v[u]));
-        const uint32_t tail = len & 15u;  // the last workgroup also owns the ragged bytes
-        if (tail && blockIdx.x == gridDim.x - 1 && tid < tail)
-            Mem<uint32_t>::st<0>(dst, nvec * 16 + tid,
-                                 gf_mulc(t, Mem<uint32_t>::ld<0>(src, nvec * 16 + tid)));
-    } else {
-        const uint32_t b1 = min(len, (blockIdx.x + 1) * VPB * 16u);
-        for (uint32_t b = blockIdx.x * VPB * 16u + tid; b < b1; b += NTHR)
-            Mem<uint32_t>::st<0>(dst, b, gf_mulc(t, Mem<uint32_t>::ld<0>(src, b)));
-    }
-}
 
 // ------------------------------------------------------------ launchers
 
@@ -1795,7 +283,7 @@ using EncCfg = Cfg<kLanes * SPLIT, U, pol_aux(2, 18), MAP, 0, WAVES, SPLIT>;
 // costs 2-3% at 4+1 / 8+2 x 64 and 128 KiB, so the smaller k keep stripe order.
 constexpr int enc_map(int k) { return k >= 16 && enc_split(k) == 1 ? 3 : 0; }
 // Reconstruct load policy: 2 = non-temporal buffer loads as in the encode
-// (production), -1 = non-temporal global loads.  Round 1 measured the global form
+// (production), -1 = non-temporal global loads.  An earlier build measured the global form
 // 1.8% faster at 8+2 x 64 KiB, when the pointer table came through per-lane loads
 // and every buffer access paid a readfirstlane loop; with the pointers in SGPRs
 // the buffer form wins by 0.5-1.1% at every width (8+2 x 64 KiB dual 405.5 vs

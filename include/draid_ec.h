@@ -2,8 +2,8 @@
  * draid_ec.h -- C ABI of the MI355X erasure-coding engine (libdraid_ec.so).
  *
  * Drop-in boundary for the parity hot path of kyleshu/draid-spdk's RAID
- * bdev modules (module/bdev/raid/).  Two nested surfaces, as SURVEY.md §8b
- * describes:
+ * bdev modules (module/bdev/raid/).  Two nested surfaces, the two the reference
+ * itself has:
  *
  *  1. The isa-l v2.30 arithmetic ABI the raid modules call (raid.h /
  *     gf_vect_mul.h), re-implemented as HIP kernels on gfx950.  Same argument

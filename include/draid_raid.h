@@ -5,7 +5,7 @@
  * raid5_simple.c): array geometry, parity placement, mapping a stripe request
  * onto chunks, slicing the parent I/O's iovecs per chunk, and the full-stripe
  * write / degraded read drivers that hand the parity arithmetic to the GPU
- * through a draid_ec_ctx.  A real SPDK module wraps these
+ * through a draid_ec_ctx.  A real SPDK module (draid-spdk_amd/spdk/raid_gpu.c) wraps these
  * calls with spdk_bdev_io / io_channel / poller glue; everything here is plain C
  * on host memory that the GPU can reach (registered or device memory).
  */
@@ -47,7 +47,7 @@ int draid_raid_start(struct draid_raid *r, int level, int num_base_bdevs, uint32
                      uint32_t strip_size_blocks, uint64_t min_base_blockcnt);
 
 /* Parity placement.  RAID5: p = (n-1) - s mod n (raid5.c:1006-1007).  RAID6
- * (undefined by the reference, DESIGN.md §8): p as RAID5, q = (p+1) mod n.
+ * (undefined by the reference): p as RAID5, q = (p+1) mod n.
  * Data indices fill the remaining disks in ascending order. */
 void draid_raid_parity_chunks(const struct draid_raid *r, uint64_t stripe, int *p, int *q);
 int draid_raid_data_disk(const struct draid_raid *r, uint64_t stripe, int data_idx);

@@ -4,7 +4,7 @@
  *
  * Config 1 is "RAID5 4+1 full-stripe write, 64KiB strip, bdevperf over malloc
  * bdevs on CPU (isa-l reference path, no GPU)": bdevperf -w write -o 262144 -q 32
- * -t 10 over a raid5 bdev of 5 malloc bdevs (SURVEY.md §8d).  bdevperf needs
+ * -t 10 over a raid5 bdev of 5 malloc bdevs.  bdevperf needs
  * SPDK + DPDK + isa-l, none of which can be built here, so this harness performs
  * the same per-request data movement on one core:
  *   - stripe index advances sequentially (bdevperf -w write is sequential);

@@ -3,7 +3,7 @@
  *
  * This is a plain-C restatement of the parity arithmetic the reference
  * (kyleshu/draid-spdk, an SPDK v22.01-pre fork) reaches through isa-l v2.30.0
- * (`isa-l/` submodule, EMPTY in the reference tree -- see SURVEY.md §8c), plus
+ * (`isa-l/` submodule, EMPTY in the reference tree), plus
  * the reference's own RAID5 geometry.  It is the checker for the HIP engine:
  * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
  * it.  The product path (draid-spdk_amd/) never links or calls it.

@@ -4,7 +4,7 @@ Second, independent path next to the C restatement in ``isal_oracle.c``:
 it builds GF(2^8) products by carry-less "Russian peasant" multiplication
 (no log/antilog tables, no Horner form) so a shared mistake between the two
 restatements is unlikely.  Semantics follow isa-l v2.30.0 as the reference
-uses it (SURVEY.md Appendix A):
+uses it:
 
 * ``xor_gen``  -- P = XOR_j D_j                     (raid5_simple.c:154,176)
 * ``pq_gen``   -- P = XOR_j D_j, Q = XOR_j 2^j D_j  (gf_vect_mul.c:152-169)

@@ -33,7 +33,7 @@ def test_c_harness_gpu(ec):
 
 
 def test_c_sanitizers():
-    """the host code under sanitizers.  The host RAID layer and
+    """The host code under sanitizers.  The host RAID layer and
     stripe cache (compiled from source into the harness) under ASan + UBSan
     and under TSan (the 8-thread stripe-cache test), and the oracle's round
     trips under ASan + UBSan -- host paths only, no GPU."""

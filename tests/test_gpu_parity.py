@@ -464,7 +464,7 @@ def test_full_size_roundtrip(ec, k, m, L, B):
 # ------------------------------------------------------------ edge buffers
 
 def _edge_stripes(k, m, L):
-    """SURVEY.md §8(d) edge buffers: all-0x00, all-0xFF, one set bit per stripe
+    """Edge buffers: all-0x00, all-0xFF, one set bit per stripe
     (every bit position and every data strip), and the raid5_ut_ref pattern
     (0xFF fill + 8-byte LE block index, raid5_ut_ref.c:324-330)."""
     n = k + m

@@ -4,10 +4,10 @@
  * driven the way an SPDK raid module on libdraid_ec would run them.
  *
  * The reference workload is bdevperf -w write -o 262144 -q 32 over a raid5 bdev
- * of 5 malloc bdevs (SURVEY.md §8d); bdevperf itself needs SPDK + DPDK + isa-l and
+ * of 5 malloc bdevs; bdevperf itself needs SPDK + DPDK + isa-l and
  * is not buildable here, and oracle/bdevperf_raid5.c is its CPU counterpart (parity
  * by the isa-l xor_gen restatement on the reactor core).  Here the same requests
- * take the module path of INTEGRATION.md §3 on one "reactor" thread:
+ * take the raid module's path through the host layer on one "reactor" thread:
  *   - user buffers and parity buffers are host memory registered once
  *     (draid_ec_host_register, as spdk_dma_malloc hugepages would be) and handed
  *     to the engine through their device addresses (draid_ec_host_device_pointer);

@@ -1,7 +1,7 @@
 /*
  * rebuild_bench.c -- rebuilding failed disks of a RAID6 array held in HBM.
  *
- * The reference has no rebuild or resync (SURVEY.md §5); its degraded read
+ * The reference has no rebuild or resync; its degraded read
  * (raid5_complete_reconstructed_stripe_request, raid5.c:544-594) rebuilds one
  * request's range.  On the GPU a whole failed disk is one batched reconstruct:
  * draid_raid_strip_table gives every stripe's rotated pointers,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate the golden fixtures under tests/golden/ (committed with this script).
 
-Sources of truth, in order of strength (SURVEY.md §8c):
+Sources of truth, in order of strength:
 
 1. ``gf_vect_mul.c`` scenarios (examples/bdev/gf_vect_mul/gf_vect_mul.c:68-347):
    glibc ``srand(0x1234)`` + ``rand()`` inputs drawn in the example's exact call
@@ -42,7 +42,7 @@ def sha(b: np.ndarray) -> str:
 
 
 def stripe_seed(s: int, j: int) -> int:
-    """Seed of strip j of stripe s (documented in DESIGN.md)."""
+    """Seed of strip j of stripe s (a fixed function of s and j, so the fixture can be regenerated)."""
     return (0x1234 ^ (s << 16) ^ j) & 0xFFFFFFFFFFFFFFFF
 
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""PCIe-inclusive rate of the host-resident stripe path (DESIGN.md §7).
+"""PCIe-inclusive rate of the host-resident stripe path.
 
 Stripes live in pinned host memory (what SPDK's registered hugepage buffers
 are); by default draid_ec_host_encode / _reconstruct read the strips
