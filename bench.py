@@ -282,7 +282,7 @@ def run_single_process(args, torch, ec) -> None:
     print(json.dumps(out), flush=True)
 
 
-COMPILED_K = tuple(range(2, 17))  # widths with unrolled kernels
+COMPILED_K = tuple(range(2, 21))  # widths with unrolled kernels
 
 
 def main() -> None:

@@ -296,7 +296,7 @@ using RecCfg = Cfg<kLanes * SPLIT, U, pol_aux(DRAID_REC_LOAD_AUX, 18), 0, DRAID_
 template <int U>
 using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global nt
 
-// Waves per SIMD of the run-time-width kernels (k > 16; kRtBlock loads per wave and
+// Waves per SIMD of the run-time-width kernels (k > 20; kRtBlock loads per wave and
 // block), same-box A/B of whole library builds, microseconds per launch
 // (profiles/r02/occupancy/runtime_width_waves.jsonl): encode 18+2 x 64 KiB x 2048
 // stripes 409 at 3, 414 at 4, 423 at 5, 431 at 6, 444 at 2; 32+2 x 1024 stripes 353 /
@@ -310,7 +310,8 @@ using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global
 #endif
 // k values with a fully unrolled instantiation; others use the runtime-k loop.
 #define DRAID_FOR_EACH_K(X) \
-    X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+    X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
+    X(17) X(18) X(19) X(20)
 
 template <int M, class Ptrs>
 static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,

@@ -195,7 +195,7 @@ def test_gf_vect_mul_any_table_any_length(ec, L):
 
 
 @pytest.mark.parametrize("k,m", [(2, 1), (4, 1), (8, 1), (16, 1), (8, 2), (9, 2), (10, 2), (12, 2), (14, 2),
-                                 (16, 2), (40, 2)])
+                                 (16, 2), (18, 2), (20, 1), (40, 2)])
 def test_recover_every_failure_set(ec, k, m):
     L = 4096
     rng = np.random.default_rng(k)
@@ -286,7 +286,7 @@ CONFIGS = [  # (k, m, strip bytes, stripes) -- BASELINE.json configs at reduced 
     (16, 2, 262144, 16),
     (14, 2, 4096, 33),
     (11, 2, 4096 + 48, 7),   # odd width, ragged length
-    (17, 2, 4096 + 48, 7),   # run-time width: one full block of 8 strips and a ragged top block
+    (21, 2, 4096 + 48, 7),   # run-time width: two full blocks of 8 strips and a ragged top block
     (24, 1, 2048, 9),        # run-time width, whole blocks only
     (33, 2, 1024 + 7, 5),    # run-time width, five blocks, byte tail
     (6, 1, 1000, 5),         # ragged length, odd size
@@ -530,7 +530,7 @@ def test_full_size_linearity(ec, k, m, L, B):
 
 # ------------------------------------------------------------ items shared by several waves
 
-SPLIT_K = [5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16]   # stripe widths whose items are dealt over 2 or 4 waves
+SPLIT_K = [5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20]   # stripe widths whose items are dealt over 2 or 4 waves
 
 
 @pytest.mark.parametrize("m", [1, 2])
