@@ -212,7 +212,8 @@ constexpr int rec_waves(int k, int m)
 {
     return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
            : m == 1             ? rec_waves_raid5(k)
-           : k <= 4             ? 0
+           : k <= 3             ? 7  // 3+2 dual 429 vs 453 us at the compiler's choice
+           : k == 4             ? 0
            : k == 5             ? 6
            : k == 6             ? 5
            : k <= 12            ? 4
