@@ -1,8 +1,9 @@
-"""Is the slow encode of a power-of-two stripe pitch (6+2 x 64 KiB = 512 KiB) a WRITE
-hot spot?  The encode writes P and Q at the same offset of every stripe; the
-reconstruct writes wherever the lost strips are.  Times the reconstruct with the same
-lost pair in every stripe against a random pair per stripe, beside the encode, for a
-padded and an unpadded pitch.  One JSON line per case."""
+"""Why a power-of-two stripe pitch (6+2 x 64 KiB = 512 KiB) encodes slowly: a WRITE hot
+spot on one address bit.  The encode writes P and Q at the same offset of every stripe;
+a reconstruct with the same lost pair in every stripe writes two chosen strips of every
+period.  Times such reconstructs for pairs inside one 256 KiB half of the period and
+pairs that straddle it, beside the encode and a random pair per stripe, for an unpadded
+and a padded pitch.  One JSON line per pitch."""
 import json
 import os
 import sys
@@ -44,7 +45,13 @@ for pad in (0, 16384):
     rand = np.stack([rng.permutation(k)[:2] for _ in range(B)]).astype(np.uint8)
     f_same = torch.from_numpy(same.reshape(-1)).to(dev)
     f_rand = torch.from_numpy(rand.reshape(-1)).to(dev)
-    out = {"shape": "6+2 x 64 KiB x 5120", "stripe_pad": pad,
+    extra = {}
+    for name, pair in (("pq", [k, k + 1]), ("first_two", [0, 1]), ("last_two_data", [k - 2, k - 1]),
+                       ("0_2", [0, 2]), ("0_4", [0, 4]), ("2_3", [2, 3]), ("1_3", [1, 3]),
+                       ("3_4", [3, 4]), ("2_q", [2, k + 1])):
+        f = torch.from_numpy(np.tile(np.array(pair, np.uint8), (B, 1)).reshape(-1)).to(dev)
+        extra[f"reconstruct_{name}_us"] = round(timed(lambda f=f: ec.reconstruct(batch, f, st)), 1)
+    out = {"shape": "6+2 x 64 KiB x 5120", "stripe_pad": pad, **extra,
            "encode_us": round(timed(lambda: ec.encode(batch, st)), 1),
            "reconstruct_same_pair_us": round(timed(lambda: ec.reconstruct(batch, f_same, st)), 1),
            "reconstruct_random_pair_us": round(timed(lambda: ec.reconstruct(batch, f_rand, st)), 1)}
