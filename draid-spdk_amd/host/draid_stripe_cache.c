@@ -86,6 +86,14 @@ static void hash_remove(struct draid_stripe_cache *c, struct entry *e)
     e->hash_next = NULL;
 }
 
+uint64_t draid_stripe_slot_bytes(uint32_t n, uint64_t strip_bytes)
+{
+    const uint64_t b = (uint64_t)n * strip_bytes;
+
+    /* strips of 256 KiB and more put P and Q into different halves by themselves */
+    return (strip_bytes <= (128u << 10) && (b % (512u << 10)) == 0) ? b + (16u << 10) : b;
+}
+
 int draid_stripe_cache_create(draid_stripe_cache **out, uint32_t nslots)
 {
     if (!out || nslots == 0)

@@ -236,6 +236,21 @@ static void test_fail_table(void)
 }
 
 /* Stripe cache and request queue (raid5.c:1047-1131, 485-521). */
+static void test_stripe_slot_bytes(void)
+{
+    /* plain n * strip unless that is a multiple of 512 KiB */
+    CHECK(draid_stripe_slot_bytes(10, 65536) == 10u * 65536);
+    CHECK(draid_stripe_slot_bytes(5, 65536) == 5u * 65536);
+    CHECK(draid_stripe_slot_bytes(18, 262144) == 18u * 262144);
+    CHECK(draid_stripe_slot_bytes(8, 65536) == 8u * 65536 + 16384);
+    CHECK(draid_stripe_slot_bytes(16, 65536) == 16u * 65536 + 16384);
+    CHECK(draid_stripe_slot_bytes(4, 131072) == 4u * 131072 + 16384);
+    CHECK(draid_stripe_slot_bytes(6, 4096) == 6u * 4096);
+    CHECK(draid_stripe_slot_bytes(128, 4096) == 128u * 4096 + 16384);
+    CHECK(draid_stripe_slot_bytes(4, 262144) == 4u * 262144);   /* P and Q a half each */
+    printf("ok stripe slot stride\n");
+}
+
 static void test_stripe_cache(void)
 {
     draid_stripe_cache *c;
@@ -760,6 +775,7 @@ int main(int argc, char **argv)
     test_mapping();
     test_stripe_asm();
     test_fail_table();
+    test_stripe_slot_bytes();
     test_stripe_cache();
     test_stripe_cache_threads();
     printf("host logic: %s\n", g_fail ? "FAIL" : "ok");
