@@ -265,6 +265,7 @@ constexpr int enc_split_waves(int k, int m)
            : enc_split(k) == 1  ? enc_waves(k)
            : (k == 8 && m == 2) ? 7
            : (m == 1 && (k == 4 || k == 5)) ? 5
+           : k >= 17            ? 5  // 18+2 394-396 vs 398-399 us at 6, 403 at 7
                                 : 6;
 }
 constexpr int rec_split_waves(int k, int m)
