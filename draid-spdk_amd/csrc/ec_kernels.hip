@@ -566,9 +566,14 @@ static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t tstrid
 {
     if (nwork == 0)
         return hipSuccess;
-    hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                       TablePtrs{tab, tstride}, k, work_src<C>(seg_len, work, ulen), fail,
-                       fstride, nwork);
+    if constexpr (C::SPLIT > 1)
+        hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                           TablePtrs{tab, tstride}, work_src<C>(seg_len, work, ulen), fail,
+                           fstride, nwork);
+    else
+        hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                           TablePtrs{tab, tstride}, k, work_src<C>(seg_len, work, ulen), fail,
+                           fstride, nwork);
     return hipGetLastError();
 }
 
@@ -614,6 +619,15 @@ hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* tabl
     }
 }
 
+// The scatter-gather reconstruct divides its items like the batched one: two waves
+// and the column division from k = 8 (DRAID_REC_WORK_COLS=0: one wave per item at
+// every width, for A/B).
+#ifndef DRAID_REC_WORK_COLS
+#define DRAID_REC_WORK_COLS 1
+#endif
+#define DRAID_REC_WORK_SPLIT(K) (DRAID_REC_WORK_COLS ? rec_split(K) : 1)
+#define DRAID_REC_WORK_WAVES(K, M) \
+    (DRAID_REC_WORK_COLS ? rec_split_waves(K, M) : rec_waves(K, M))
 hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
                                    uint32_t tstride, const uint32_t* seg_len, const uint8_t* fail,
                                    uint32_t fstride, const void* work, uint32_t ulen,
@@ -622,9 +636,11 @@ hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const*
     switch (k) {
 #define DRAID_CASE(K)                                                                         \
     case K:                                                                                   \
-        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K), rec_waves(K, 1)>>(    \
+        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K), DRAID_REC_WORK_WAVES(K, 1), \
+                                                         DRAID_REC_WORK_SPLIT(K)>>(             \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st) \
-                      : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K), rec_waves(K, 2)>>(    \
+                      : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K), DRAID_REC_WORK_WAVES(K, 2), \
+                                                         DRAID_REC_WORK_SPLIT(K)>>(             \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE

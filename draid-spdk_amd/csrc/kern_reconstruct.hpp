@@ -38,9 +38,9 @@ struct RecPlan {
 // memory instruction, and an item whose first instruction waits a full memory
 // round trip before the plan is known, and only then issues its strip loads,
 // takes half as long again.
-__device__ __forceinline__ uint32_t load_fail_pair(const uint8_t* fail, uint32_t s)
+__device__ __forceinline__ uint32_t load_fail_pair_at(const uint8_t* pair)
 {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(fail) + 2 * static_cast<uintptr_t>(s);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(pair);
     // constant address space: the table is input only, never written by the kernel
     typedef const uint32_t __attribute__((address_space(4)))* ccw;
     const ccw w = (ccw)(a & ~static_cast<uintptr_t>(3));
@@ -49,6 +49,10 @@ __device__ __forceinline__ uint32_t load_fail_pair(const uint8_t* fail, uint32_t
     if (at == 3u)  // the pair straddles two words (a table at an odd address)
         v |= w[1] << 8;
     return v & 0xffffu;
+}
+__device__ __forceinline__ uint32_t load_fail_pair(const uint8_t* fail, uint32_t s)
+{
+    return load_fail_pair_at(fail + 2 * static_cast<size_t>(s));
 }
 
 // Decodes the (wave-uniform) failure pair: which strips are lost, which
@@ -613,18 +617,55 @@ __device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, Rec
     }
 }
 
+// Chunk c of stripe (or segment) s with its failure pair decoded: the 16-byte vectors
+// through the column path, a byte tail and unaligned strips on wave 0's byte path.
+template <int KT, int M, class C, class Ptrs>
+__device__ __forceinline__ void reconstruct_item_cols(const Ptrs& pp, uint32_t s, uint32_t c,
+                                                      uint32_t len, uint32_t cps, RecPlan& pl,
+                                                      bool aligned, ColLds<KT>& lds)
+{
+    constexpr int SPLIT = C::SPLIT, POL = C::POL;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t nvec = len >> 4;
+    auto none = [](RecPlan&) {};
+    if (aligned) {
+        const uint32_t i = c * 64u + lane;
+        if ((c + 1) * 64u <= nvec) {
+            if (M == 2 && !pl.needq)
+                recover_cols_vec<KT, M, SPLIT, POL, false, false>(pp, s, pl, w, lane, i, nvec, lds);
+            else
+                recover_cols_vec<KT, M, SPLIT, POL, false, true>(pp, s, pl, w, lane, i, nvec, lds);
+        } else {
+            recover_cols_vec<KT, M, SPLIT, POL, true, true>(pp, s, pl, w, lane, i, nvec, lds);
+        }
+        const uint32_t tail = len & 15u;
+        if (w == 0 && tail && c == cps - 1 && lane < tail)
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl,
+                                                                   nvec * 16 + lane, 64, len, none);
+    } else if (w == 0) {
+        const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
+        pl.t1 = mul.t1;
+        pl.t2 = mul.t2;
+        const uint32_t b1 = min(len, (c + 1) * 1024u);
+        for (uint32_t b = c * 1024u + lane; b < b1; b += 64)
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, b, 64, b1, none);
+    }
+}
+
 template <int KT, int M, class C, class Ptrs>
 __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_cols(
     Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, const uint8_t* fail, uint32_t f01,
     uint32_t* bad, ItemGrid ig)
 {
     static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one shared item per workgroup, stripe order");
-    constexpr int SPLIT = C::SPLIT, POL = C::POL;
     __shared__ ColLds<KT> lds;
     uint32_t c, s;
     ig.coords(c, s);
     if (s >= nstripes)
         return;
+    // The pointer row and the failure pair are independent scalar reads: both are
+    // issued before either is used, so an item pays one memory round trip for
+    // them, not two, before its strip loads can go out.
     const bool aligned = stripe_aligned<KT, M>(pp, s, KT);
     uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
     if (fail) {
@@ -634,33 +675,8 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_c
     }
     RecPlan pl = decode_failures_mask<KT, M>(f0, f1);
     const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
-    if (!pl.skip) {
-        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-        const uint32_t nvec = len >> 4;
-        auto none = [](RecPlan&) {};
-        if (aligned) {
-            const uint32_t i = c * 64u + lane;
-            if ((c + 1) * 64u <= nvec) {
-                if (M == 2 && !pl.needq)
-                    recover_cols_vec<KT, M, SPLIT, POL, false, false>(pp, s, pl, w, lane, i, nvec, lds);
-                else
-                    recover_cols_vec<KT, M, SPLIT, POL, false, true>(pp, s, pl, w, lane, i, nvec, lds);
-            } else {
-                recover_cols_vec<KT, M, SPLIT, POL, true, true>(pp, s, pl, w, lane, i, nvec, lds);
-            }
-            const uint32_t tail = len & 15u;
-            if (w == 0 && tail && c == cps - 1 && lane < tail)
-                recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl,
-                                                                       nvec * 16 + lane, 64, len, none);
-        } else if (w == 0) {
-            const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
-            pl.t1 = mul.t1;
-            pl.t2 = mul.t2;
-            const uint32_t b1 = min(len, (c + 1) * 1024u);
-            for (uint32_t b = c * 1024u + lane; b < b1; b += 64)
-                recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, b, 64, b1, none);
-        }
-    }
+    if (!pl.skip)
+        reconstruct_item_cols<KT, M, C>(pp, s, c, len, cps, pl, aligned, lds);
     if (count_bad)
         atomicAdd(bad, 1u);
 }

@@ -117,6 +117,24 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_w
     }
 }
 
+// The column reconstruct over a segment list: one workgroup per work item.  The
+// failure pair rides at a row stride beside the segment's pointers.
+template <int KT, int M, class C>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_work_cols(
+    TablePtrs pp, WorkSrc ws, const uint8_t* fail, uint32_t fstride, uint32_t nwork)
+{
+    static_assert(KT > 0 && C::SPLIT > 1, "shared items need a compile-time width");
+    constexpr uint32_t CB = static_cast<uint32_t>(C::ITEM) * C::U * 16;
+    __shared__ ColLds<KT> lds;
+    uint32_t seg, chunk, len, cps;
+    ws.get(blockIdx.x, CB, seg, chunk, len, cps);
+    const bool aligned = stripe_aligned<KT, M>(pp, seg, KT);  // pointer row and pair read together
+    const uint32_t f = load_fail_pair_at(fail + static_cast<size_t>(fstride) * seg);
+    RecPlan pl = decode_failures_mask<KT, M>(f & 0xffu, f >> 8);
+    if (!pl.skip)  // uniform across the workgroup
+        reconstruct_item_cols<KT, M, C>(pp, seg, chunk, len, cps, pl, aligned, lds);
+}
+
 // ------------------------------------------------------------ read-modify-write
 
 // Small-write parity update (raid5_stripe_write_preread_complete_rmw,
