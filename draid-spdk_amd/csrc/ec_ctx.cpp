@@ -76,7 +76,10 @@ private:
 };
 
 struct Group {
-    Group(int op_, uint32_t k_, uint32_t m_) : op(op_), k(k_), m(m_), w(k_ + m_ + (op_ == 1)) {}
+    Group(int op_, uint32_t k_, uint32_t m_, uint32_t level_)
+        : op(op_), level(level_), k(k_), m(m_), w(k_ + m_ + (op_ == 1))
+    {
+    }
     Group(const Group&) = delete;
     Group& operator=(const Group&) = delete;
     ~Group()
@@ -86,6 +89,7 @@ struct Group {
                 (void)hipEventDestroy(e);
     }
     int op;  // 0 encode, 1 reconstruct, 2 read-modify-write update
+    uint32_t level;  // fences in front of its segments within their requests (draid_ec_ctx_fence)
     uint64_t first_seq = 0;         // queue position of the batch's first segment in this group
     uint32_t k, m;                  // op 2: k = 2 * touched chunks (old/new list pairs)
     uint32_t w;                     // pointer slots per segment: k+m, +1 for op 1
@@ -148,6 +152,12 @@ struct draid_ec_ctx {
     static constexpr uint64_t kTickets = 64;
     hipEvent_t ticket_ev[kTickets] = {};
     uint64_t ticket_next = 1, ticket_done = 0;
+    // draid_ec_ctx_mark / rollback: segments per group when the mark was set, and
+    // how many launches had happened (a launch since then makes it stale).
+    std::vector<size_t> mark_nseg;
+    uint64_t mark_seq = 0, mark_launches = 0, launches = 0;
+    bool marked = false;
+    uint32_t level = 0;  // segments queued now go to groups of this level
 };
 
 namespace {
@@ -233,9 +243,9 @@ const uint32_t* address_order(draid_ec_ctx* c, const Group& g)
 Group& group_for(draid_ec_ctx* c, int op, uint32_t k, uint32_t m)
 {
     for (Group& g : c->groups)
-        if (g.op == op && g.k == k && g.m == m)
+        if (g.op == op && g.k == k && g.m == m && g.level == c->level)
             return g;
-    c->groups.emplace_back(op, k, m);
+    c->groups.emplace_back(op, k, m, c->level);
     return c->groups.back();
 }
 
@@ -397,7 +407,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
         ++c->queued_segments;
         remaining -= run;
     }
-    if (c->autoflush && g.len.size() >= c->autoflush) {
+    // (a group behind a fence waits for the flush: its predecessors must launch first)
+    if (c->autoflush && g.level == 0 && g.len.size() >= c->autoflush) {
         DeviceGuard on(c->device);
         const int rc = flush_group(c, g);
         recount(c);
@@ -567,6 +578,7 @@ int flush_group(draid_ec_ctx* c, Group& g)
     const size_t nseg = g.len.size();
     if (nseg == 0)
         return 0;
+    ++c->launches;
     if (nseg == 1 && g.op != 2 && g.k + g.m <= static_cast<uint32_t>(draid::kMaxArgPtrs))
         return flush_single(c, g);
     const size_t per_seg = g.w * sizeof(void*) + sizeof(uint32_t) + 2 * sizeof(uint32_t);
@@ -766,8 +778,9 @@ int draid_ec_ctx_flush(draid_ec_ctx* c)
     if (!c)
         return ctx_arg("ctx is NULL");
     DeviceGuard on(c->device);
-    // Groups launch in the order their first segment of this batch was queued
-    // (a group object outlives its batches, so creation order says nothing).
+    // Groups launch level by level (draid_ec_ctx_fence), and within a level in
+    // the order their first segment of this batch was queued (a group object
+    // outlives its batches, so creation order says nothing).
     Group* order[64];
     std::vector<Group*> many;
     size_t n = 0;
@@ -783,11 +796,14 @@ int draid_ec_ctx_flush(draid_ec_ctx* c)
             ++n;
         }
     Group** gp = many.empty() ? order : many.data();
-    std::sort(gp, gp + n, [](const Group* a, const Group* b) { return a->first_seq < b->first_seq; });
+    std::sort(gp, gp + n, [](const Group* a, const Group* b) {
+        return a->level != b->level ? a->level < b->level : a->first_seq < b->first_seq;
+    });
     int rc = 0;
     for (size_t i = 0; i < n && rc == 0; ++i)
         rc = flush_group(c, *gp[i]);
     recount(c);  // on failure: exactly the segments that did not launch
+    c->level = 0;
     return rc;
 }
 
@@ -885,6 +901,56 @@ int draid_ec_ctx_discard_queued(draid_ec_ctx* c)
         g.fail.clear();
     }
     c->queued_segments = 0;
+    return 0;
+}
+
+int draid_ec_ctx_mark(draid_ec_ctx* c)
+{
+    if (!c)
+        return ctx_arg("ctx is NULL");
+    c->mark_nseg.resize(c->groups.size());
+    size_t i = 0;
+    for (const Group& g : c->groups)
+        c->mark_nseg[i++] = g.len.size();
+    c->mark_seq = c->seq;
+    c->mark_launches = c->launches;
+    c->marked = true;
+    c->level = 0;  // a request starts in front of every fence
+    return 0;
+}
+
+int draid_ec_ctx_fence(draid_ec_ctx* c)
+{
+    if (!c)
+        return ctx_arg("ctx is NULL");
+    ++c->level;
+    return 0;
+}
+
+int draid_ec_ctx_rollback(draid_ec_ctx* c)
+{
+    if (!c)
+        return ctx_arg("ctx is NULL");
+    if (!c->marked)
+        return ctx_arg("rollback without a mark");
+    c->marked = false;
+    if (c->launches != c->mark_launches)
+        return ctx_arg("rollback: segments queued since the mark have been launched");
+    size_t i = 0;
+    for (Group& g : c->groups) {  // groups are only ever appended: index i is stable
+        const size_t keep = i < c->mark_nseg.size() ? c->mark_nseg[i] : 0;
+        ++i;
+        const size_t have = g.len.size();
+        if (have <= keep)
+            continue;
+        const size_t nmeta = g.fail.size() / have;
+        g.ptrs.shrink(keep * g.w);
+        g.len.resize(keep);
+        g.fail.resize(keep * nmeta);
+    }
+    c->seq = c->mark_seq;
+    c->level = 0;
+    recount(c);
     return 0;
 }
 

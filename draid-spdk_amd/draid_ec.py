@@ -41,6 +41,7 @@ EXPORTS = (
     "draid_ec_pointer_cache_flush", "draid_ec_ctx_flush_ticket", "draid_ec_ctx_ticket_query",
     "draid_ec_ctx_set_host_pointers", "draid_ec_host_alloc", "draid_ec_host_free",
     "draid_ec_ctx_discard_queued", "draid_ec_device_current",
+    "draid_ec_ctx_mark", "draid_ec_ctx_rollback", "draid_ec_ctx_fence",
     "draid_ec_shard_of", "draid_ec_shard_range", "draid_ec_shard_count",
     "draid_ec_mgpu_create", "draid_ec_mgpu_destroy", "draid_ec_mgpu_devices",
     "draid_ec_mgpu_device", "draid_ec_mgpu_stream", "draid_ec_mgpu_encode",
@@ -149,7 +150,8 @@ def lib() -> C.CDLL:
         L.draid_ec_set_variant.argtypes = [i32]
         L.draid_ec_ctx_create.argtypes = [C.POINTER(vp)]
         for f in ("draid_ec_ctx_destroy", "draid_ec_ctx_flush", "draid_ec_ctx_query",
-                  "draid_ec_ctx_synchronize"):
+                  "draid_ec_ctx_synchronize", "draid_ec_ctx_mark", "draid_ec_ctx_rollback",
+                  "draid_ec_ctx_fence"):
             getattr(L, f).argtypes = [vp]
         L.draid_ec_ctx_stream.argtypes = [vp]
         L.draid_ec_ctx_stream.restype = vp
@@ -400,6 +402,15 @@ class Ctx:
 
     def queued(self):
         return lib().draid_ec_ctx_queued(self.h)
+
+    def mark(self) -> int:
+        return _check(lib().draid_ec_ctx_mark(self.h), "ctx_mark")
+
+    def rollback(self) -> int:
+        return _check(lib().draid_ec_ctx_rollback(self.h), "ctx_rollback")
+
+    def fence(self) -> int:
+        return _check(lib().draid_ec_ctx_fence(self.h), "ctx_fence")
 
     def flush_ticket(self) -> int:
         t = C.c_uint64()

@@ -79,8 +79,23 @@ struct rg_info {
 	draid_stripe_cache *stripes;	/* per-stripe request queue, shared by the channels */
 	int ngpus;			/* slots: contexts per channel, stripe s on slot s mod ngpus */
 	int ndevices;			/* GPUs the slots are dealt over */
+	int refs;			/* the raid bdev (until stop) + every open channel */
+	bool stopped;			/* stop has run: new requests fail, running ones finish */
 	struct raid_gpu_stats stats;
 };
+
+/* The framework stops a level module as soon as the array leaves the online
+ * state -- on a hot-remove that is while channels are open and requests in
+ * flight (raid_bdev_deconfigure, bdev_raid.c:1267-1289) -- so what the requests
+ * use lives until the last channel is gone. */
+static void
+rg_info_put(struct rg_info *info)
+{
+	if (__atomic_sub_fetch(&info->refs, 1, __ATOMIC_ACQ_REL) == 0) {
+		draid_stripe_cache_destroy(info->stripes);
+		free(info);
+	}
+}
 
 #define RG_COUNT(info, field) __atomic_fetch_add(&(info)->stats.field, 1, __ATOMIC_RELAXED)
 
@@ -136,6 +151,7 @@ struct rg_channel {
 	struct spdk_poller *poller;
 	struct rg_request *requests;
 	uint8_t *pool;			/* RG_MAX_REQUESTS * n strip buffers */
+	bool pool_registered;		/* this channel registered the pool with the GPU runtime */
 	TAILQ_HEAD(, rg_request) free_reqs;
 	TAILQ_HEAD(, rg_request) queued;	/* parity work queued on a context, not flushed */
 	TAILQ_HEAD(, rg_request) running;	/* flushed: waiting for the ticket */
@@ -158,8 +174,9 @@ rg_degraded_mask(const struct raid_bdev *raid_bdev)
 	uint32_t mask = 0;
 	uint8_t i;
 
+	/* the flags are written on whichever thread sees a disk fail */
 	for (i = 0; i < raid_bdev->num_base_bdevs; i++) {
-		if (raid_bdev->base_bdev_info[i].degraded) {
+		if (__atomic_load_n(&raid_bdev->base_bdev_info[i].degraded, __ATOMIC_ACQUIRE)) {
 			mask |= 1u << i;
 		}
 	}
@@ -168,25 +185,66 @@ rg_degraded_mask(const struct raid_bdev *raid_bdev)
 
 /* The reference's fault-injection hook (bdev_raid.c:1157-1170, commented out
  * there) as a function: marks a base bdev degraded or healthy again. */
+static pthread_mutex_t g_degraded_lock = PTHREAD_MUTEX_INITIALIZER;
+
 int
 raid_gpu_set_degraded(struct raid_bdev *raid_bdev, uint8_t slot, bool degraded)
 {
-	uint8_t i;
-	bool any = false;
+	uint32_t mask;
+	int rc = 0;
 
 	if (slot >= raid_bdev->num_base_bdevs) {
 		return -EINVAL;
 	}
-	if (degraded && !raid_bdev->base_bdev_info[slot].degraded &&
-	    __builtin_popcount(rg_degraded_mask(raid_bdev)) >=
-	    raid_bdev->module->base_bdevs_max_degraded) {
-		return -EBUSY;	/* one more than the level tolerates */
+	/* two channels' threads may see two different disks fail at the same time:
+	 * the "one more than the level tolerates" test and the update are one step */
+	pthread_mutex_lock(&g_degraded_lock);
+	mask = rg_degraded_mask(raid_bdev);
+	if (degraded && !(mask & (1u << slot)) &&
+	    __builtin_popcount(mask) >= raid_bdev->module->base_bdevs_max_degraded) {
+		rc = -EBUSY;
+	} else {
+		mask = degraded ? mask | (1u << slot) : mask & ~(1u << slot);
+		__atomic_store_n(&raid_bdev->base_bdev_info[slot].degraded, degraded, __ATOMIC_RELEASE);
+		__atomic_store_n(&raid_bdev->degraded, mask != 0, __ATOMIC_RELEASE);
 	}
-	raid_bdev->base_bdev_info[slot].degraded = degraded;
-	for (i = 0; i < raid_bdev->num_base_bdevs; i++) {
-		any |= raid_bdev->base_bdev_info[i].degraded;
+	pthread_mutex_unlock(&g_degraded_lock);
+	return rc;
+}
+
+/* What a hot-remove handler calls for an online array of this module instead of
+ * taking the whole array offline (raid_bdev_remove_base_bdev -> raid_bdev_deconfigure,
+ * bdev_raid.c:1333-1365): the removed base bdev becomes a degraded disk.  New
+ * requests plan around it from the next submit on; requests that already have
+ * I/O on it see that I/O fail or succeed and are redone if it failed.  The base
+ * bdev's descriptor and channels stay open until the array is deleted (the
+ * framework releases them in raid_bdev_destruct, bdev_raid.c:285-323, for every
+ * base bdev whose removal is scheduled), so the removed bdev's own unregister
+ * completes only then. */
+int
+raid_gpu_base_bdev_removed(struct raid_bdev *raid_bdev, struct raid_base_bdev_info *base_info)
+{
+	const long slot = base_info - raid_bdev->base_bdev_info;
+	int rc;
+
+	if (raid_bdev->module == NULL || raid_bdev->module->submit_rw_request != rg_submit_rw_request) {
+		return -ENOTSUP;	/* another level module's array */
 	}
-	raid_bdev->degraded = any;
+	if (raid_bdev->state != RAID_BDEV_STATE_ONLINE || raid_bdev->destruct_called ||
+	    raid_bdev->module_private == NULL) {
+		return -ENODEV;		/* not serving I/O: let the framework clean up */
+	}
+	if (slot < 0 || slot >= raid_bdev->num_base_bdevs) {
+		return -EINVAL;
+	}
+	rc = raid_gpu_set_degraded(raid_bdev, (uint8_t)slot, true);
+	if (rc != 0) {
+		SPDK_ERRLOG("base bdev %ld of %s removed: more failures than %s tolerates\n", slot,
+			    raid_bdev->bdev.name, rg_level_name(raid_bdev));
+		return rc;
+	}
+	SPDK_NOTICELOG("base bdev %ld of %s removed: the array stays online, degraded\n", slot,
+		       raid_bdev->bdev.name);
 	return 0;
 }
 
@@ -223,6 +281,7 @@ rg_complete(struct rg_request *req, enum spdk_bdev_io_status status)
 			if (nreq->thread == spdk_get_thread()) {
 				rg_start_request(nreq);
 			} else {
+				RG_COUNT(info, handoffs);
 				spdk_thread_send_msg(nreq->thread, _rg_start_request, nreq);
 			}
 		}
@@ -376,6 +435,24 @@ rg_queue_error(struct rg_request *req, int rc, const char *what)
 	return rc;
 }
 
+/* A request's parity work is queued whole or not at all: it may take several
+ * queueing calls (rebuild then re-encode; one update per touched range), and a
+ * later call can fail (a parent iovec the GPU cannot reach) after earlier ones
+ * queued segments on this request's strip buffers and the parent's iovecs.  The
+ * request is then failed and its buffers reused, so those segments must not
+ * run. */
+static int
+rg_queue_failed(struct rg_request *req, draid_ec_ctx *ctx, int rc, const char *what)
+{
+	rg_queue_error(req, rc, what);
+	if (draid_ec_ctx_rollback(ctx) != 0) {
+		/* cannot happen without autoflush; never leave a dangling segment */
+		SPDK_ERRLOG("stripe %" PRIu64 ": rollback failed: %s\n", req->sreq.stripe_index,
+			    draid_ec_last_error());
+	}
+	return rc;
+}
+
 /* Queues the parity work of a write whose prereads (if any) are in, and lists
  * its base writes in ios[]. */
 static int
@@ -385,6 +462,7 @@ rg_queue_write(struct rg_request *req)
 	draid_ec_ctx *ctx = req->ch->ctx[req->gpu];
 	int nw = 0, rc;
 
+	draid_ec_ctx_mark(ctx);
 	if (req->kind == RG_WRITE_FULL) {
 		void *parity[2] = { req->chunk_buf[req->sreq.p_disk],
 				    req->sreq.q_disk >= 0 ? req->chunk_buf[req->sreq.q_disk] : NULL
@@ -393,7 +471,7 @@ rg_queue_write(struct rg_request *req)
 		rc = draid_raid_stripe_write(&req->geom, ctx, &req->sreq, bdev_io->u.bdev.iovs,
 					     bdev_io->u.bdev.iovcnt, parity, req->ios, &nw);
 		if (rc) {
-			return rg_queue_error(req, rc, "draid_raid_stripe_write");
+			return rg_queue_failed(req, ctx, rc, "draid_raid_stripe_write");
 		}
 	} else {
 		if (req->kind == RG_WRITE_DEGRADED) {
@@ -403,8 +481,11 @@ rg_queue_write(struct rg_request *req)
 			rc = draid_raid_stripe_degraded_rebuild(&req->geom, ctx, req->sreq.stripe_index,
 								req->chunk_buf);
 			if (rc) {
-				return rg_queue_error(req, rc, "draid_raid_stripe_degraded_rebuild");
+				return rg_queue_failed(req, ctx, rc, "draid_raid_stripe_degraded_rebuild");
 			}
+			/* the encode below reads the rebuilt strips: it must not share a launch
+			 * with encodes other requests queued ahead of this rebuild */
+			draid_ec_ctx_fence(ctx);
 			memset(&req->plan, 0, sizeof(req->plan));
 			req->plan.mode = DRAID_WRITE_RCW;
 			req->plan.p_offset = 0;
@@ -414,7 +495,7 @@ rg_queue_write(struct rg_request *req)
 						     bdev_io->u.bdev.iovs, bdev_io->u.bdev.iovcnt,
 						     req->chunk_buf, req->ios, &nw);
 		if (rc) {
-			return rg_queue_error(req, rc, "draid_raid_stripe_write_partial");
+			return rg_queue_failed(req, ctx, rc, "draid_raid_stripe_write_partial");
 		}
 	}
 	req->nio = nw;
@@ -475,11 +556,15 @@ rg_phase_done(struct rg_request *req)
 		if (req->kind == RG_READ) {
 			/* the surviving ranges are in: rebuild the lost requested range */
 			struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(req->raid_io);
-			int rc = draid_raid_stripe_read_rebuild(&req->geom, req->ch->ctx[req->gpu],
-								&req->sreq, bdev_io->u.bdev.iovs,
-								bdev_io->u.bdev.iovcnt, req->chunk_buf);
+			draid_ec_ctx *ctx = req->ch->ctx[req->gpu];
+			int rc;
+
+			draid_ec_ctx_mark(ctx);
+			rc = draid_raid_stripe_read_rebuild(&req->geom, ctx, &req->sreq,
+							    bdev_io->u.bdev.iovs, bdev_io->u.bdev.iovcnt,
+							    req->chunk_buf);
 			if (rc) {
-				rg_queue_error(req, rc, "draid_raid_stripe_read_rebuild");
+				rg_queue_failed(req, ctx, rc, "draid_raid_stripe_read_rebuild");
 				rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
 				return;
 			}
@@ -606,10 +691,16 @@ rg_submit_rw_request(struct raid_bdev_io *raid_io)
 {
 	struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(raid_io);
 	struct rg_channel *ch = raid_bdev_io_channel_get_resource(raid_io->raid_ch);
-	struct rg_info *info = raid_io->raid_bdev->module_private;
+	struct rg_info *info = ch->info;	/* module_private is gone once the module stopped */
 	struct rg_request *req;
 	int rc;
 
+	if (spdk_unlikely(info->stopped)) {
+		/* the array went offline (a base bdev was removed, or it is being
+		 * deleted) with this channel still open */
+		raid_bdev_io_complete(raid_io, SPDK_BDEV_IO_STATUS_FAILED);
+		return;
+	}
 	req = TAILQ_FIRST(&ch->free_reqs);
 	if (spdk_unlikely(req == NULL)) {
 		/* all stripe requests in flight: retry when one completes
@@ -754,8 +845,18 @@ rg_io_channel_resource_deinit(void *resource)
 		ch->requests = NULL;
 	}
 	if (ch->pool) {
+		if (ch->pool_registered) {
+			/* drops the pinning and the library's cached translation of the range,
+			 * so a later allocation at these addresses is looked up afresh */
+			draid_ec_host_unregister(ch->pool);
+			ch->pool_registered = false;
+		}
 		spdk_dma_free(ch->pool);
 		ch->pool = NULL;
+	}
+	if (ch->info) {
+		rg_info_put(ch->info);
+		ch->info = NULL;
 	}
 }
 
@@ -774,6 +875,7 @@ rg_io_channel_resource_init(struct raid_bdev *raid_bdev, void *resource)
 
 	memset(ch, 0, sizeof(*ch));
 	ch->info = info;
+	__atomic_add_fetch(&info->refs, 1, __ATOMIC_RELAXED);
 	TAILQ_INIT(&ch->free_reqs);
 	TAILQ_INIT(&ch->queued);
 	TAILQ_INIT(&ch->running);
@@ -793,11 +895,14 @@ rg_io_channel_resource_init(struct raid_bdev *raid_bdev, void *resource)
 		void *dev_ptr;
 
 		if (draid_ec_device_pointer(ch->pool, (size_t)RG_MAX_REQUESTS * n * strip_bytes,
-					    &dev_ptr) != 0 &&
-		    draid_ec_host_register(ch->pool, (size_t)RG_MAX_REQUESTS * n * strip_bytes) != 0) {
-			SPDK_ERRLOG("strip buffers are not GPU reachable and cannot be registered: %s\n",
-				    draid_ec_last_error());
-			goto err;
+					    &dev_ptr) != 0) {
+			if (draid_ec_host_register(ch->pool,
+						   (size_t)RG_MAX_REQUESTS * n * strip_bytes) != 0) {
+				SPDK_ERRLOG("strip buffers are not GPU reachable and cannot be "
+					    "registered: %s\n", draid_ec_last_error());
+				goto err;
+			}
+			ch->pool_registered = true;
 		}
 	}
 	for (i = 0; i < RG_MAX_REQUESTS; i++) {
@@ -861,6 +966,7 @@ rg_start(struct raid_bdev *raid_bdev)
 		return -ENOMEM;
 	}
 	info->raid_bdev = raid_bdev;
+	info->refs = 1;
 	RAID_FOR_EACH_BASE_BDEV(raid_bdev, base_info) {
 		min_blockcnt = spdk_min(min_blockcnt, base_info->bdev->blockcnt);
 	}
@@ -908,9 +1014,9 @@ rg_stop(struct raid_bdev *raid_bdev)
 	struct rg_info *info = raid_bdev->module_private;
 
 	if (info) {
-		draid_stripe_cache_destroy(info->stripes);
-		free(info);
 		raid_bdev->module_private = NULL;
+		__atomic_store_n(&info->stopped, true, __ATOMIC_RELEASE);
+		rg_info_put(info);	/* freed with the last channel */
 	}
 }
 

@@ -17,6 +17,18 @@
  * exceed the level's base_bdevs_max_degraded. */
 int raid_gpu_set_degraded(struct raid_bdev *raid_bdev, uint8_t slot, bool degraded);
 
+/* For the framework's hot-remove path: turns the removal of `base_info`'s bdev
+ * into a degraded disk of an online array of this module, where the reference
+ * takes the array offline (raid_bdev_remove_base_bdev, bdev_raid.c:1333-1365).
+ * The patch is one statement in front of that function's raid_bdev_deconfigure
+ * call:
+ *	if (raid_gpu_base_bdev_removed(raid_bdev, base_info) == 0) { return; }
+ * Returns 0 when the array stays online (the caller returns); -EBUSY when the
+ * level cannot tolerate one more lost disk, -ENOTSUP for another module's array,
+ * -ENODEV when the array is not online -- the caller then goes on to
+ * raid_bdev_deconfigure as before. */
+int raid_gpu_base_bdev_removed(struct raid_bdev *raid_bdev, struct raid_base_bdev_info *base_info);
+
 /* What the module has done on a raid bdev since it started (diagnostics and
  * tests; summed over the channels). */
 struct raid_gpu_stats {
@@ -27,6 +39,8 @@ struct raid_gpu_stats {
 	uint64_t reads;			/* reads served by plain base reads */
 	uint64_t degraded_reads;	/* reads that rebuilt a lost requested range */
 	uint64_t redone;		/* requests redone after a base bdev failed under them */
+	uint64_t handoffs;		/* a stripe handed to a request of another thread
+					 * (spdk_thread_send_msg, as raid5.c:501-505) */
 	uint64_t flushes;		/* launches: one per poller iteration with queued work */
 	uint64_t gpu_requests;		/* requests whose parity work those launches carried */
 };

@@ -227,11 +227,14 @@ int draid_ec_ctx_update_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m, uint32_t n
  * is called.
  * Order: segments queued with the same (op, k, m) form a group and carry no
  * order among themselves (the flush may run them in address order).  Groups
- * run in the order in which their FIRST segment of this batch was queued, on
- * one stream.  So work that depends on an earlier group's output may share a
- * batch with it (reconstruct into chunk buffers, then an encode reading them)
- * as long as the earlier group is not queued into again afterwards; any other
- * dependency needs a flush in between.
+ * run one after the other on one stream, in the order in which their FIRST
+ * segment of this batch was queued -- which says nothing about two segments of
+ * different groups once several requests share a batch (request A's encode
+ * opens the encode group, request B then queues a rebuild and an encode that
+ * reads the rebuilt strips: B's encode would run with A's, ahead of B's
+ * rebuild).  Work that reads what earlier work of the same request writes
+ * therefore puts a draid_ec_ctx_fence() between the two; any dependency on
+ * work of an EARLIER flush is already ordered by the stream.
  * On failure (a piece's descriptor memory, the work-item limit, a launch
  * error) the pieces launched so far keep running, every segment that did not
  * launch stays queued -- draid_ec_ctx_queued() counts exactly those -- and the
@@ -259,6 +262,25 @@ uint64_t draid_ec_ctx_queued(draid_ec_ctx *ctx);   /* segments queued since last
 /* Drops every queued segment (after a failed flush whose requests the caller
  * fails instead of retrying).  Work already launched is not affected. */
 int draid_ec_ctx_discard_queued(draid_ec_ctx *ctx);
+/* All-or-nothing queueing of a request that takes several queueing calls (a
+ * degraded write: rebuild, then re-encode; an RMW over several ranges).
+ * draid_ec_ctx_mark remembers what is queued now; draid_ec_ctx_rollback drops
+ * every segment queued since, in every group, and leaves the earlier ones as
+ * they were -- so a request whose n-th call fails (an unreachable iovec) leaves
+ * nothing behind that a later flush would run on buffers it no longer owns.
+ * One mark at a time; rollback returns 1 without a mark, or when something was
+ * launched since the mark (a flush, or autoflush: those segments are running). */
+int draid_ec_ctx_mark(draid_ec_ctx *ctx);
+int draid_ec_ctx_rollback(draid_ec_ctx *ctx);
+/* Segments queued from now on (until the next draid_ec_ctx_mark, rollback or
+ * flush) run after every segment queued in this batch before their request's
+ * fence: a request that rebuilds lost strips into its buffers and then encodes
+ * over them calls mark, queues the rebuild, calls fence, queues the encode.
+ * Requests stay batched: all work in front of a fence shares launches per
+ * (op, k, m) as before, all work behind one fence likewise; the flush runs the
+ * first kind, then the second (then work behind a second fence, ...).
+ * Autoflush never launches work behind a fence early. */
+int draid_ec_ctx_fence(draid_ec_ctx *ctx);
 
 /* Launch an (op, k, m) group as soon as it holds `segments` queued segments,
  * from inside the queueing call (0 = only at draid_ec_ctx_flush, the default).

@@ -144,7 +144,11 @@ int draid_raid_stripe_degraded_read(const struct draid_raid *r, draid_ec_ctx *ct
  * draid_raid_stripe_degraded_read with ctx = NULL lists the reads only; once they
  * are in, draid_raid_stripe_degraded_rebuild queues the reconstruct on ctx.  (With
  * a ctx the one call does both: right when the reads are ordered before the
- * flush, e.g. copies on the ctx's stream.) */
+ * flush, e.g. copies on the ctx's stream.)  Work queued afterwards that reads the
+ * rebuilt strips -- the re-encode of a degraded partial write -- goes behind a
+ * draid_ec_ctx_fence(ctx): several requests may share the batch, and without
+ * the fence that encode would launch with the encodes queued before this
+ * rebuild. */
 int draid_raid_stripe_degraded_rebuild(const struct draid_raid *r, draid_ec_ctx *ctx,
                                        uint64_t stripe, void *const *chunk_buf);
 

@@ -67,7 +67,7 @@ task_done(struct spdk_bdev_io *bdev_io, bool success, void *cb_arg)
 	struct task *t = cb_arg;
 	struct job *j = t->job;
 
-	free(bdev_io);
+	spdk_bdev_free_io(bdev_io);
 	j->outstanding--;
 	j->done++;
 	if (!success) {

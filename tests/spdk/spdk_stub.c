@@ -1,5 +1,5 @@
 /*
- * spdk_stub.c -- a single-threaded stand-in for the parts of the SPDK runtime that
+ * spdk_stub.c -- a stand-in for the parts of the SPDK runtime that
  * module/bdev/raid uses, so that the reference's raid framework (bdev_raid.c,
  * compiled from /root/reference where it lies) and a raid level module can be
  * linked and driven in a test process without libspdk / DPDK.
@@ -8,14 +8,26 @@
  * ut_multithread.c play for the reference's own unit tests
  * (test/unit/lib/bdev/raid/bdev_raid.c/bdev_raid_ut.c:39-42,104-139), but does
  * real work where the I/O path needs it:
- *   - bdev registry, open/close/claim, io_device + io_channel with per-channel
- *     context buffers (spdk/thread.h semantics, one thread);
- *   - RAM base bdevs whose reads and writes complete asynchronously, from
- *     stub_poll(), with -ENOMEM and I/O error injection;
+ *   - SPDK threads (test/common/lib/ut_multithread.c:78,200 allocate_threads /
+ *     set_thread / poll_threads): up to STUB_MAX_THREADS of them, each with its own
+ *     message ring, pollers, io_wait queue, base-bdev completions and io_channels;
+ *     spdk_get_thread() is the current one.  They can be stepped round-robin from
+ *     one OS thread (the ut_multithread way, deterministic interleaving) or each
+ *     be run by an OS thread of its own (the message ring is the only structure
+ *     another thread writes, and it is locked);
+ *   - bdev registry, open/close/claim, remove events and the deferred destruct of
+ *     spdk_bdev_unregister (lib/bdev/bdev.c:5850-5947: open descriptors are told
+ *     SPDK_BDEV_EVENT_REMOVE on their own thread, the bdev is destructed when the
+ *     last one closes), io_device + one io_channel per (device, thread);
+ *   - RAM base bdevs whose reads and writes complete asynchronously, on the
+ *     submitting thread, with -ENOMEM and I/O error injection; a no-copy mode
+ *     (what module/bdev/null does) for measuring the layers above;
  *   - the bdev layer's submit path for the raid bdev: spdk_bdev_io allocation
  *     with the module's driver context, splitting at optimal_io_boundary with
  *     spdk_bdev_io_get_split_parent(), parent completion;
- *   - pollers, thread messages, io_wait queues, mempools, DMA memory.
+ *   - pollers, io_wait queues, mempools, DMA memory;
+ *   - counts of what is still allocated (I/Os, descriptors, channels, pollers,
+ *     messages, DMA blocks), for leak checks.
  * DMA memory (spdk_dma_malloc) comes from the GPU runtime's pinned allocator
  * (draid_ec_host_alloc): in a deployment SPDK's hugepage memory is registered with
  * the GPU once; the pool this runs on refuses hipHostRegister, and allocating
@@ -42,7 +54,7 @@ static int g_log_level = 0;
 static int g_error_count;
 
 void stub_set_log_level(int level) { g_log_level = level; }
-int stub_error_count(void) { return g_error_count; }
+int stub_error_count(void) { return __atomic_load_n(&g_error_count, __ATOMIC_RELAXED); }
 
 void
 spdk_log(enum spdk_log_level level, const char *file, const int line, const char *func,
@@ -51,7 +63,7 @@ spdk_log(enum spdk_log_level level, const char *file, const int line, const char
 	va_list ap;
 
 	if (level == SPDK_LOG_ERROR) {
-		g_error_count++;
+		__atomic_fetch_add(&g_error_count, 1, __ATOMIC_RELAXED);
 	}
 	if ((int)level > g_log_level) {
 		return;
@@ -91,6 +103,24 @@ int spdk_json_write_named_array_begin(struct spdk_json_write_ctx *w, const char 
 int spdk_json_write_named_object_begin(struct spdk_json_write_ctx *w, const char *n)
 { (void)w; (void)n; return 0; }
 
+/* ------------------------------------------------------------ what is still allocated */
+
+static struct stub_live g_live;
+
+#define LIVE_ADD(field, d) __atomic_fetch_add(&g_live.field, (d), __ATOMIC_RELAXED)
+
+void
+stub_live(struct stub_live *out)
+{
+	out->ios = __atomic_load_n(&g_live.ios, __ATOMIC_RELAXED);
+	out->descs = __atomic_load_n(&g_live.descs, __ATOMIC_RELAXED);
+	out->channels = __atomic_load_n(&g_live.channels, __ATOMIC_RELAXED);
+	out->pollers = __atomic_load_n(&g_live.pollers, __ATOMIC_RELAXED);
+	out->msgs = __atomic_load_n(&g_live.msgs, __ATOMIC_RELAXED);
+	out->dma = __atomic_load_n(&g_live.dma, __ATOMIC_RELAXED);
+	out->io_devices = __atomic_load_n(&g_live.io_devices, __ATOMIC_RELAXED);
+}
+
 /* ------------------------------------------------------------ DMA memory, mempools */
 
 static bool g_plain_dma;
@@ -128,6 +158,7 @@ spdk_dma_malloc(size_t size, size_t align, uint64_t *phys_addr)
 	h = (struct dma_hdr *)p - 1;
 	h->raw = raw;
 	h->pinned = !g_plain_dma;
+	LIVE_ADD(dma, 1);
 	return p;
 }
 
@@ -151,6 +182,7 @@ spdk_dma_free(void *buf)
 		return;
 	}
 	h = (struct dma_hdr *)buf - 1;
+	LIVE_ADD(dma, -1);
 	if (h->pinned) {
 		draid_ec_host_free(h->raw);
 	} else {
@@ -229,42 +261,113 @@ spdk_mempool_free(struct spdk_mempool *mp)
 	}
 }
 
-/* ------------------------------------------------------------ thread, messages, pollers */
-
-struct spdk_thread {
-	int id;
-};
-static struct spdk_thread g_thread = { 1 };
+/* ------------------------------------------------------------ threads, messages, pollers */
 
 struct stub_msg {
 	spdk_msg_fn fn;
 	void *ctx;
 	TAILQ_ENTRY(stub_msg) link;
 };
-static TAILQ_HEAD(, stub_msg) g_msgs = TAILQ_HEAD_INITIALIZER(g_msgs);
 
 struct spdk_poller {
 	spdk_poller_fn fn;
 	void *arg;
 	bool dead;
+	struct spdk_thread *thread;
 	TAILQ_ENTRY(spdk_poller) link;
 };
-static TAILQ_HEAD(, spdk_poller) g_pollers = TAILQ_HEAD_INITIALIZER(g_pollers);
 
-struct spdk_thread *spdk_get_thread(void) { return &g_thread; }
+/* One SPDK thread (lib/thread/thread.c:972 spdk_thread_poll drains the same
+ * things in the same order: messages, then pollers).  Only `msgs` is touched by
+ * other threads. */
+struct spdk_thread {
+	int id;
+	pthread_mutex_t lock;
+	TAILQ_HEAD(, stub_msg) msgs;
+	TAILQ_HEAD(, spdk_poller) pollers;
+	TAILQ_HEAD(, spdk_bdev_io) completions;		/* base bdev I/O submitted here */
+	TAILQ_HEAD(, spdk_bdev_io_wait_entry) io_wait;
+	struct stub_thread_stats stats;
+};
+
+static struct spdk_thread g_threads[STUB_MAX_THREADS];
+static int g_nthreads = 1;
+static __thread struct spdk_thread *t_thread;
+
+__attribute__((constructor)) static void
+stub_threads_init(void)
+{
+	int i;
+
+	for (i = 0; i < STUB_MAX_THREADS; i++) {
+		struct spdk_thread *t = &g_threads[i];
+
+		t->id = i;
+		pthread_mutex_init(&t->lock, NULL);
+		TAILQ_INIT(&t->msgs);
+		TAILQ_INIT(&t->pollers);
+		TAILQ_INIT(&t->completions);
+		TAILQ_INIT(&t->io_wait);
+	}
+}
+
+struct spdk_thread *spdk_get_thread(void) { return t_thread ? t_thread : &g_threads[0]; }
+
+int
+stub_allocate_threads(int num_threads)
+{
+	if (num_threads < 1 || num_threads > STUB_MAX_THREADS) {
+		return -EINVAL;
+	}
+	g_nthreads = num_threads;
+	return 0;
+}
+
+int stub_num_threads(void) { return g_nthreads; }
+
+void
+stub_set_thread(int id)
+{
+	assert(id >= 0 && id < g_nthreads);
+	t_thread = &g_threads[id];
+}
+
+int stub_thread_id(const struct spdk_thread *thread) { return thread->id; }
+
+void
+stub_thread_stats(int id, struct stub_thread_stats *out, bool reset)
+{
+	struct spdk_thread *t = &g_threads[id];
+
+	pthread_mutex_lock(&t->lock);
+	if (out) {
+		*out = t->stats;
+	}
+	if (reset) {
+		memset(&t->stats, 0, sizeof(t->stats));
+	}
+	pthread_mutex_unlock(&t->lock);
+}
 
 int
 spdk_thread_send_msg(const struct spdk_thread *thread, spdk_msg_fn fn, void *ctx)
 {
+	struct spdk_thread *t = (struct spdk_thread *)thread;
 	struct stub_msg *m = calloc(1, sizeof(*m));
 
-	(void)thread;
 	if (!m) {
 		return -ENOMEM;
 	}
 	m->fn = fn;
 	m->ctx = ctx;
-	TAILQ_INSERT_TAIL(&g_msgs, m, link);
+	LIVE_ADD(msgs, 1);
+	pthread_mutex_lock(&t->lock);
+	TAILQ_INSERT_TAIL(&t->msgs, m, link);
+	t->stats.msgs++;
+	if (t != spdk_get_thread()) {
+		t->stats.msgs_from_other_threads++;
+	}
+	pthread_mutex_unlock(&t->lock);
 	return 0;
 }
 
@@ -281,7 +384,9 @@ spdk_poller_register_named(spdk_poller_fn fn, void *arg, uint64_t period_microse
 	}
 	p->fn = fn;
 	p->arg = arg;
-	TAILQ_INSERT_TAIL(&g_pollers, p, link);
+	p->thread = spdk_get_thread();
+	TAILQ_INSERT_TAIL(&p->thread->pollers, p, link);
+	LIVE_ADD(pollers, 1);
 	return p;
 }
 
@@ -295,7 +400,13 @@ void
 spdk_poller_unregister(struct spdk_poller **ppoller)
 {
 	if (ppoller && *ppoller) {
-		(*ppoller)->dead = true;	/* freed by stub_poll, which may be iterating */
+		/* only its own thread may touch a poller (lib/thread/thread.c:1607-1628) */
+		if ((*ppoller)->thread != spdk_get_thread()) {
+			fprintf(stderr, "stub: poller of thread %d unregistered from thread %d\n",
+				(*ppoller)->thread->id, spdk_get_thread()->id);
+			abort();
+		}
+		(*ppoller)->dead = true;	/* freed by that thread's poll, which may be iterating */
 		*ppoller = NULL;
 	}
 }
@@ -306,15 +417,19 @@ struct io_device {
 	void *io_device;
 	spdk_io_channel_create_cb create_cb;
 	spdk_io_channel_destroy_cb destroy_cb;
+	spdk_io_device_unregister_cb unregister_cb;
 	uint32_t ctx_size;
-	struct spdk_io_channel *ch;	/* the one thread's channel */
+	struct spdk_io_channel *ch[STUB_MAX_THREADS];	/* one per thread */
+	int nch;
 	bool unregistered;
 	TAILQ_ENTRY(io_device) link;
 };
 static TAILQ_HEAD(, io_device) g_io_devices = TAILQ_HEAD_INITIALIZER(g_io_devices);
+static pthread_mutex_t g_io_devices_lock = PTHREAD_MUTEX_INITIALIZER;
 
 struct spdk_io_channel {
 	struct io_device *dev;
+	struct spdk_thread *thread;
 	int ref;
 };
 SPDK_STATIC_ASSERT(sizeof(struct spdk_io_channel) <= SPDK_IO_CHANNEL_STRUCT_SIZE,
@@ -325,12 +440,14 @@ io_device_find(void *io_device)
 {
 	struct io_device *d;
 
+	pthread_mutex_lock(&g_io_devices_lock);
 	TAILQ_FOREACH(d, &g_io_devices, link) {
 		if (d->io_device == io_device && !d->unregistered) {
-			return d;
+			break;
 		}
 	}
-	return NULL;
+	pthread_mutex_unlock(&g_io_devices_lock);
+	return d;
 }
 
 void
@@ -345,15 +462,31 @@ spdk_io_device_register(void *io_device, spdk_io_channel_create_cb create_cb,
 	d->create_cb = create_cb;
 	d->destroy_cb = destroy_cb;
 	d->ctx_size = ctx_size;
+	pthread_mutex_lock(&g_io_devices_lock);
 	TAILQ_INSERT_TAIL(&g_io_devices, d, link);
+	pthread_mutex_unlock(&g_io_devices_lock);
+	LIVE_ADD(io_devices, 1);
 }
 
+/* The device goes away once it is unregistered and its last channel is released
+ * (lib/thread/thread.c:2029-2095); its unregister callback runs then. */
 static void
 io_device_release(struct io_device *d)
 {
-	if (d->unregistered && d->ch == NULL) {
+	bool gone;
+
+	pthread_mutex_lock(&g_io_devices_lock);
+	gone = d->unregistered && d->nch == 0;
+	if (gone) {
 		TAILQ_REMOVE(&g_io_devices, d, link);
+	}
+	pthread_mutex_unlock(&g_io_devices_lock);
+	if (gone) {
+		if (d->unregister_cb) {
+			d->unregister_cb(d->io_device);
+		}
 		free(d);
+		LIVE_ADD(io_devices, -1);
 	}
 }
 
@@ -365,10 +498,8 @@ spdk_io_device_unregister(void *io_device, spdk_io_device_unregister_cb unregist
 	if (!d) {
 		return;
 	}
+	d->unregister_cb = unregister_cb;
 	d->unregistered = true;
-	if (unregister_cb) {
-		unregister_cb(io_device);
-	}
 	io_device_release(d);
 }
 
@@ -376,26 +507,30 @@ struct spdk_io_channel *
 spdk_get_io_channel(void *io_device)
 {
 	struct io_device *d = io_device_find(io_device);
+	struct spdk_thread *t = spdk_get_thread();
 	struct spdk_io_channel *ch;
 
 	if (!d) {
 		return NULL;
 	}
-	if (d->ch) {
-		d->ch->ref++;
-		return d->ch;
+	if (d->ch[t->id]) {
+		d->ch[t->id]->ref++;
+		return d->ch[t->id];
 	}
 	ch = calloc(1, SPDK_IO_CHANNEL_STRUCT_SIZE + d->ctx_size);
 	if (!ch) {
 		return NULL;
 	}
 	ch->dev = d;
+	ch->thread = t;
 	ch->ref = 1;
 	if (d->create_cb(io_device, spdk_io_channel_get_ctx(ch)) != 0) {
 		free(ch);
 		return NULL;
 	}
-	d->ch = ch;
+	d->ch[t->id] = ch;
+	__atomic_fetch_add(&d->nch, 1, __ATOMIC_RELAXED);
+	LIVE_ADD(channels, 1);
 	return ch;
 }
 
@@ -404,13 +539,23 @@ spdk_put_io_channel(struct spdk_io_channel *ch)
 {
 	struct io_device *d = ch->dev;
 
+	/* a channel belongs to the thread that got it (lib/thread/thread.c:2250-2267) */
+	if (ch->thread != spdk_get_thread()) {
+		fprintf(stderr, "stub: channel of thread %d released from thread %d\n", ch->thread->id,
+			spdk_get_thread()->id);
+		abort();
+	}
 	assert(ch->ref > 0);
 	if (--ch->ref > 0) {
 		return;
 	}
 	d->destroy_cb(d->io_device, spdk_io_channel_get_ctx(ch));
-	d->ch = NULL;
+	d->ch[ch->thread->id] = NULL;
+	pthread_mutex_lock(&g_io_devices_lock);
+	d->nch--;
+	pthread_mutex_unlock(&g_io_devices_lock);
 	free(ch);
+	LIVE_ADD(channels, -1);
 	io_device_release(d);
 }
 
@@ -420,12 +565,17 @@ spdk_io_channel_from_ctx(void *ctx)
 	return (struct spdk_io_channel *)((uint8_t *)ctx - SPDK_IO_CHANNEL_STRUCT_SIZE);
 }
 
+struct spdk_thread *spdk_io_channel_get_thread(struct spdk_io_channel *ch) { return ch->thread; }
+
 /* ------------------------------------------------------------ bdev registry */
 
 struct spdk_bdev_desc {
 	struct spdk_bdev *bdev;
 	spdk_bdev_event_cb_t event_cb;
 	void *event_ctx;
+	struct spdk_thread *thread;	/* the opener's: remove events are delivered there */
+	int refs;			/* remove notifications in flight */
+	bool closed;
 	TAILQ_ENTRY(spdk_bdev_desc) link;
 };
 
@@ -463,21 +613,76 @@ spdk_bdev_register(struct spdk_bdev *bdev)
 	}
 	TAILQ_INIT(&bdev->internal.open_descs);
 	bdev->internal.claim_module = NULL;
+	bdev->internal.status = SPDK_BDEV_STATUS_READY;
+	bdev->internal.unregister_cb = NULL;
 	TAILQ_INSERT_TAIL(&g_bdevs, bdev, internal.link);
 	return 0;
 }
 
+/* bdev_fini (lib/bdev/bdev.c:5826-5847): destruct, then the unregister callback. */
+static void
+bdev_fini(struct spdk_bdev *bdev)
+{
+	spdk_bdev_unregister_cb cb = bdev->internal.unregister_cb;
+	void *ctx = bdev->internal.unregister_ctx;
+	int rc = 0;
+
+	if (bdev->fn_table && bdev->fn_table->destruct) {
+		rc = bdev->fn_table->destruct(bdev->ctxt);	/* may free the bdev */
+	}
+	if (cb) {
+		cb(ctx, rc);
+	}
+}
+
+static void
+remove_notify(void *arg)
+{
+	struct spdk_bdev_desc *desc = arg;
+
+	desc->refs--;
+	if (!desc->closed) {
+		desc->event_cb(SPDK_BDEV_EVENT_REMOVE, desc->bdev, desc->event_ctx);
+	} else if (desc->refs == 0) {
+		free(desc);
+		LIVE_ADD(descs, -1);
+	}
+}
+
+static int
+notify_open_descs(struct spdk_bdev *bdev)
+{
+	struct spdk_bdev_desc *desc;
+	int n = 0;
+
+	TAILQ_FOREACH(desc, &bdev->internal.open_descs, link) {
+		if (desc->event_cb) {
+			desc->refs++;
+			spdk_thread_send_msg(desc->thread, remove_notify, desc);
+		}
+		n++;
+	}
+	return n;
+}
+
+/* spdk_bdev_unregister (lib/bdev/bdev.c:5850-5947): every open descriptor gets
+ * SPDK_BDEV_EVENT_REMOVE as a message on its own thread; the bdev is destructed
+ * when the last of them closes (at once if none is open). */
 void
 spdk_bdev_unregister(struct spdk_bdev *bdev, spdk_bdev_unregister_cb cb_fn, void *cb_arg)
 {
-	int rc = 0;
-
-	TAILQ_REMOVE(&g_bdevs, bdev, internal.link);
-	if (bdev->fn_table && bdev->fn_table->destruct) {
-		rc = bdev->fn_table->destruct(bdev->ctxt);
+	if (bdev->internal.status == SPDK_BDEV_STATUS_REMOVING) {
+		if (cb_fn) {
+			cb_fn(cb_arg, -EBUSY);
+		}
+		return;
 	}
-	if (cb_fn) {
-		cb_fn(cb_arg, rc);
+	bdev->internal.status = SPDK_BDEV_STATUS_REMOVING;
+	bdev->internal.unregister_cb = cb_fn;
+	bdev->internal.unregister_ctx = cb_arg;
+	TAILQ_REMOVE(&g_bdevs, bdev, internal.link);	/* no new opens by name */
+	if (notify_open_descs(bdev) == 0) {
+		bdev_fini(bdev);
 	}
 }
 
@@ -499,7 +704,9 @@ spdk_bdev_open_ext(const char *bdev_name, bool write, spdk_bdev_event_cb_t event
 	desc->bdev = bdev;
 	desc->event_cb = event_cb;
 	desc->event_ctx = event_ctx;
+	desc->thread = spdk_get_thread();
 	TAILQ_INSERT_TAIL(&bdev->internal.open_descs, desc, link);
+	LIVE_ADD(descs, 1);
 	*_desc = desc;
 	return 0;
 }
@@ -507,8 +714,24 @@ spdk_bdev_open_ext(const char *bdev_name, bool write, spdk_bdev_event_cb_t event
 void
 spdk_bdev_close(struct spdk_bdev_desc *desc)
 {
-	TAILQ_REMOVE(&desc->bdev->internal.open_descs, desc, link);
-	free(desc);
+	struct spdk_bdev *bdev = desc->bdev;
+
+	/* lib/bdev/bdev.c:6092: a descriptor is closed on the thread that opened it */
+	if (desc->thread != spdk_get_thread()) {
+		fprintf(stderr, "stub: descriptor of thread %d closed from thread %d\n", desc->thread->id,
+			spdk_get_thread()->id);
+		abort();
+	}
+	TAILQ_REMOVE(&bdev->internal.open_descs, desc, link);
+	desc->closed = true;
+	if (desc->refs == 0) {
+		free(desc);
+		LIVE_ADD(descs, -1);
+	}
+	if (bdev->internal.status == SPDK_BDEV_STATUS_REMOVING &&
+	    TAILQ_EMPTY(&bdev->internal.open_descs)) {
+		bdev_fini(bdev);
+	}
 }
 
 struct spdk_bdev *spdk_bdev_desc_get_bdev(struct spdk_bdev_desc *desc) { return desc->bdev; }
@@ -529,16 +752,13 @@ void spdk_bdev_module_release_bdev(struct spdk_bdev *bdev) { bdev->internal.clai
 
 size_t spdk_bdev_get_buf_align(const struct spdk_bdev *bdev) { return (size_t)1 << bdev->required_alignment; }
 
+/* A base bdev is pulled out from under its users: what spdk_bdev_unregister of
+ * that bdev does to them (the event only; the RAM disk itself stays until
+ * stub_ram_bdev_destroy, I/O to it fails once the test marks it dead). */
 void
 stub_hot_remove(struct spdk_bdev *bdev)
 {
-	struct spdk_bdev_desc *desc, *tmp;
-
-	TAILQ_FOREACH_SAFE(desc, &bdev->internal.open_descs, link, tmp) {
-		if (desc->event_cb) {
-			desc->event_cb(SPDK_BDEV_EVENT_REMOVE, bdev, desc->event_ctx);
-		}
-	}
+	notify_open_descs(bdev);
 }
 
 /* ------------------------------------------------------------ RAM base bdevs */
@@ -546,10 +766,28 @@ stub_hot_remove(struct spdk_bdev *bdev)
 struct ram_bdev {
 	struct spdk_bdev bdev;
 	uint8_t *data;
-	int fail_next, enomem_next;
+	int fail_next, enomem_next;	/* atomics: any thread submits and completes */
 	bool dead;
+	bool null_io;			/* complete without moving data (module/bdev/null) */
 	struct stub_bdev_stats stats;
 };
+
+#define RAM_STAT(r, field, d) __atomic_fetch_add(&(r)->stats.field, (d), __ATOMIC_RELAXED)
+
+/* Takes one from a countdown of injected faults; false when none is left. */
+static bool
+take_one(int *counter)
+{
+	int v = __atomic_load_n(counter, __ATOMIC_RELAXED);
+
+	while (v > 0) {
+		if (__atomic_compare_exchange_n(counter, &v, v - 1, false, __ATOMIC_RELAXED,
+						__ATOMIC_RELAXED)) {
+			return true;
+		}
+	}
+	return false;
+}
 
 static struct spdk_bdev_module g_ram_module = { .name = "stub_ram" };
 
@@ -618,9 +856,13 @@ stub_ram_bdev_destroy(struct spdk_bdev *bdev)
 }
 
 uint8_t *stub_ram_bdev_data(struct spdk_bdev *bdev) { return ram_of(bdev)->data; }
-void stub_inject_io_error(struct spdk_bdev *bdev, int count) { ram_of(bdev)->fail_next = count; }
-void stub_inject_enomem(struct spdk_bdev *bdev, int count) { ram_of(bdev)->enomem_next = count; }
-void stub_set_dead(struct spdk_bdev *bdev, bool dead) { ram_of(bdev)->dead = dead; }
+void stub_inject_io_error(struct spdk_bdev *bdev, int count)
+{ __atomic_store_n(&ram_of(bdev)->fail_next, count, __ATOMIC_RELAXED); }
+void stub_inject_enomem(struct spdk_bdev *bdev, int count)
+{ __atomic_store_n(&ram_of(bdev)->enomem_next, count, __ATOMIC_RELAXED); }
+void stub_set_dead(struct spdk_bdev *bdev, bool dead)
+{ __atomic_store_n(&ram_of(bdev)->dead, dead, __ATOMIC_RELAXED); }
+void stub_set_null_io(struct spdk_bdev *bdev, bool null_io) { ram_of(bdev)->null_io = null_io; }
 
 void
 stub_ram_bdev_stats(struct spdk_bdev *bdev, struct stub_bdev_stats *out, bool reset)
@@ -649,21 +891,36 @@ spdk_bdev_io_type_supported(struct spdk_bdev *bdev, enum spdk_bdev_io_type io_ty
 
 /* ------------------------------------------------------------ base bdev I/O */
 
-static TAILQ_HEAD(, spdk_bdev_io) g_completions = TAILQ_HEAD_INITIALIZER(g_completions);
-static TAILQ_HEAD(, spdk_bdev_io_wait_entry) g_io_wait = TAILQ_HEAD_INITIALIZER(g_io_wait);
+void
+spdk_bdev_free_io(struct spdk_bdev_io *bdev_io)
+{
+	free(bdev_io);
+	LIVE_ADD(ios, -1);
+}
 
-void spdk_bdev_free_io(struct spdk_bdev_io *bdev_io) { free(bdev_io); }
+/* I/O goes through the submitting thread's own channel (include/spdk/bdev.h: "ch
+ * must be a channel of the calling thread"). */
+static void
+check_channel_thread(const struct spdk_io_channel *ch, const char *what)
+{
+	if (ch && ch->thread != spdk_get_thread()) {
+		fprintf(stderr, "stub: %s on thread %d through a channel of thread %d\n", what,
+			spdk_get_thread()->id, ch->thread->id);
+		abort();
+	}
+}
 
 static int
-ram_submit(struct spdk_bdev_desc *desc, enum spdk_bdev_io_type type, struct iovec *iov, int iovcnt,
-	   uint64_t offset_blocks, uint64_t num_blocks, spdk_bdev_io_completion_cb cb, void *cb_arg)
+ram_submit(struct spdk_bdev_desc *desc, struct spdk_io_channel *ch, enum spdk_bdev_io_type type,
+	   struct iovec *iov, int iovcnt, uint64_t offset_blocks, uint64_t num_blocks,
+	   spdk_bdev_io_completion_cb cb, void *cb_arg)
 {
 	struct ram_bdev *r = ram_of(desc->bdev);
 	struct spdk_bdev_io *io;
 
-	if (r->enomem_next > 0) {
-		r->enomem_next--;
-		r->stats.enomem++;
+	check_channel_thread(ch, "base bdev I/O");
+	if (take_one(&r->enomem_next)) {
+		RAM_STAT(r, enomem, 1);
 		return -ENOMEM;
 	}
 	if (type != SPDK_BDEV_IO_TYPE_RESET && offset_blocks + num_blocks > r->bdev.blockcnt) {
@@ -682,7 +939,8 @@ ram_submit(struct spdk_bdev_desc *desc, enum spdk_bdev_io_type type, struct iove
 	io->internal.cb = cb;
 	io->internal.caller_ctx = cb_arg;
 	io->internal.desc = desc;
-	TAILQ_INSERT_TAIL(&g_completions, io, internal.link);
+	LIVE_ADD(ios, 1);
+	TAILQ_INSERT_TAIL(&spdk_get_thread()->completions, io, internal.link);
 	return 0;
 }
 
@@ -691,8 +949,8 @@ spdk_bdev_readv_blocks(struct spdk_bdev_desc *desc, struct spdk_io_channel *ch, 
 		       int iovcnt, uint64_t offset_blocks, uint64_t num_blocks,
 		       spdk_bdev_io_completion_cb cb, void *cb_arg)
 {
-	(void)ch;
-	return ram_submit(desc, SPDK_BDEV_IO_TYPE_READ, iov, iovcnt, offset_blocks, num_blocks, cb, cb_arg);
+	return ram_submit(desc, ch, SPDK_BDEV_IO_TYPE_READ, iov, iovcnt, offset_blocks, num_blocks, cb,
+			  cb_arg);
 }
 
 int
@@ -700,8 +958,7 @@ spdk_bdev_writev_blocks(struct spdk_bdev_desc *desc, struct spdk_io_channel *ch,
 			int iovcnt, uint64_t offset_blocks, uint64_t num_blocks,
 			spdk_bdev_io_completion_cb cb, void *cb_arg)
 {
-	(void)ch;
-	return ram_submit(desc, SPDK_BDEV_IO_TYPE_WRITE, iov, iovcnt, offset_blocks, num_blocks, cb,
+	return ram_submit(desc, ch, SPDK_BDEV_IO_TYPE_WRITE, iov, iovcnt, offset_blocks, num_blocks, cb,
 			  cb_arg);
 }
 
@@ -709,8 +966,7 @@ int
 spdk_bdev_reset(struct spdk_bdev_desc *desc, struct spdk_io_channel *ch, spdk_bdev_io_completion_cb cb,
 		void *cb_arg)
 {
-	(void)ch;
-	return ram_submit(desc, SPDK_BDEV_IO_TYPE_RESET, NULL, 0, 0, 0, cb, cb_arg);
+	return ram_submit(desc, ch, SPDK_BDEV_IO_TYPE_RESET, NULL, 0, 0, 0, cb, cb_arg);
 }
 
 int
@@ -718,8 +974,8 @@ spdk_bdev_queue_io_wait(struct spdk_bdev *bdev, struct spdk_io_channel *ch,
 			struct spdk_bdev_io_wait_entry *entry)
 {
 	(void)bdev;
-	(void)ch;
-	TAILQ_INSERT_TAIL(&g_io_wait, entry, link);
+	check_channel_thread(ch, "io_wait");
+	TAILQ_INSERT_TAIL(&spdk_get_thread()->io_wait, entry, link);
 	return 0;
 }
 
@@ -732,17 +988,16 @@ ram_complete(struct spdk_bdev_io *io)
 	bool ok = true;
 	int i;
 
-	if (r->dead) {
+	if (__atomic_load_n(&r->dead, __ATOMIC_RELAXED)) {
 		ok = false;
-	} else if (r->fail_next > 0 && io->type != SPDK_BDEV_IO_TYPE_RESET) {
-		r->fail_next--;
+	} else if (io->type != SPDK_BDEV_IO_TYPE_RESET && take_one(&r->fail_next)) {
 		ok = false;
 	}
 	if (ok && (io->type == SPDK_BDEV_IO_TYPE_READ || io->type == SPDK_BDEV_IO_TYPE_WRITE)) {
 		uint8_t *p = r->data + io->u.bdev.offset_blocks * r->bdev.blocklen;
 		uint64_t left = io->u.bdev.num_blocks * r->bdev.blocklen;
 
-		for (i = 0; i < io->u.bdev.iovcnt && left; i++) {
+		for (i = 0; i < io->u.bdev.iovcnt && left && !r->null_io; i++) {
 			const uint64_t n = spdk_min(left, (uint64_t)io->u.bdev.iovs[i].iov_len);
 
 			if (io->type == SPDK_BDEV_IO_TYPE_READ) {
@@ -753,19 +1008,19 @@ ram_complete(struct spdk_bdev_io *io)
 			p += n;
 			left -= n;
 		}
-		if (left) {
+		if (left && !r->null_io) {
 			ok = false;	/* iovecs shorter than the block range */
 		}
 		if (io->type == SPDK_BDEV_IO_TYPE_READ) {
-			r->stats.reads++;
-			r->stats.read_blocks += io->u.bdev.num_blocks;
+			RAM_STAT(r, reads, 1);
+			RAM_STAT(r, read_blocks, io->u.bdev.num_blocks);
 		} else {
-			r->stats.writes++;
-			r->stats.write_blocks += io->u.bdev.num_blocks;
+			RAM_STAT(r, writes, 1);
+			RAM_STAT(r, write_blocks, io->u.bdev.num_blocks);
 		}
 	}
 	if (!ok) {
-		r->stats.failed++;
+		RAM_STAT(r, failed, 1);
 	}
 	io->internal.cb(io, ok, io->internal.caller_ctx);
 }
@@ -790,7 +1045,7 @@ stub_split_done(struct spdk_bdev_io *child, bool success, void *cb_arg)
 {
 	struct spdk_bdev_io *parent = cb_arg;
 
-	free(child);
+	spdk_bdev_free_io(child);
 	if (!success) {
 		parent->internal.status = SPDK_BDEV_IO_STATUS_FAILED;
 	}
@@ -829,6 +1084,7 @@ alloc_io(struct spdk_bdev *bdev, struct spdk_io_channel *ch, enum spdk_bdev_io_t
 	struct spdk_bdev_io *io = calloc(1, sizeof(*io) + (size_t)module_ctx_size(bdev));
 
 	if (io) {
+		LIVE_ADD(ios, 1);
 		io->bdev = bdev;
 		io->type = type;
 		io->u.bdev.offset_blocks = offset_blocks;
@@ -848,6 +1104,7 @@ stub_bdev_submit(struct spdk_bdev *bdev, struct spdk_io_channel *ch, enum spdk_b
 	const uint64_t boundary = bdev->optimal_io_boundary;
 	uint64_t off = offset_blocks, left = num_blocks, consumed = 0;
 
+	check_channel_thread(ch, "raid bdev I/O");
 	if (offset_blocks + num_blocks > bdev->blockcnt || num_blocks == 0) {
 		return -EINVAL;
 	}
@@ -907,58 +1164,94 @@ stub_bdev_submit(struct spdk_bdev *bdev, struct spdk_io_channel *ch, enum spdk_b
 
 /* ------------------------------------------------------------ the reactor */
 
+/* One iteration of the current thread: messages, io_wait retries, base bdev
+ * completions, pollers (spdk_thread_poll, lib/thread/thread.c:910-1010). */
 int
 stub_poll(void)
 {
+	struct spdk_thread *t = spdk_get_thread();
 	int ran = 0;
 	struct stub_msg *m;
 	struct spdk_bdev_io *io;
 	struct spdk_poller *p, *ptmp;
+	TAILQ_HEAD(, stub_msg) msgs = TAILQ_HEAD_INITIALIZER(msgs);
 	TAILQ_HEAD(, spdk_bdev_io_wait_entry) waits = TAILQ_HEAD_INITIALIZER(waits);
 	TAILQ_HEAD(, spdk_bdev_io) done = TAILQ_HEAD_INITIALIZER(done);
 	struct spdk_bdev_io_wait_entry *w;
 
-	while ((m = TAILQ_FIRST(&g_msgs)) != NULL) {
-		TAILQ_REMOVE(&g_msgs, m, link);
+	/* messages sent while these run wait for the next iteration */
+	pthread_mutex_lock(&t->lock);
+	TAILQ_SWAP(&msgs, &t->msgs, stub_msg, link);
+	pthread_mutex_unlock(&t->lock);
+	while ((m = TAILQ_FIRST(&msgs)) != NULL) {
+		TAILQ_REMOVE(&msgs, m, link);
 		m->fn(m->ctx);
 		free(m);
+		LIVE_ADD(msgs, -1);
 		ran++;
 	}
-	/* entries queued while these run wait for the next iteration */
-	TAILQ_SWAP(&waits, &g_io_wait, spdk_bdev_io_wait_entry, link);
+	TAILQ_SWAP(&waits, &t->io_wait, spdk_bdev_io_wait_entry, link);
 	while ((w = TAILQ_FIRST(&waits)) != NULL) {
 		TAILQ_REMOVE(&waits, w, link);
 		w->cb_fn(w->cb_arg);
 		ran++;
 	}
-	TAILQ_SWAP(&done, &g_completions, spdk_bdev_io, internal.link);
+	TAILQ_SWAP(&done, &t->completions, spdk_bdev_io, internal.link);
 	while ((io = TAILQ_FIRST(&done)) != NULL) {
 		TAILQ_REMOVE(&done, io, internal.link);
 		ram_complete(io);
 		ran++;
 	}
-	TAILQ_FOREACH_SAFE(p, &g_pollers, link, ptmp) {
+	TAILQ_FOREACH_SAFE(p, &t->pollers, link, ptmp) {
 		if (!p->dead && p->fn(p->arg) > 0) {
 			ran++;
 		}
 	}
-	TAILQ_FOREACH_SAFE(p, &g_pollers, link, ptmp) {
+	TAILQ_FOREACH_SAFE(p, &t->pollers, link, ptmp) {
 		if (p->dead) {
-			TAILQ_REMOVE(&g_pollers, p, link);
+			TAILQ_REMOVE(&t->pollers, p, link);
 			free(p);
+			LIVE_ADD(pollers, -1);
 		}
 	}
 	return ran;
 }
 
-bool
-stub_poll_until(volatile int *done, double seconds)
+int
+stub_poll_thread(int id)
+{
+	struct spdk_thread *saved = t_thread;
+	int ran;
+
+	stub_set_thread(id);
+	ran = stub_poll();
+	t_thread = saved;
+	return ran;
+}
+
+int
+stub_poll_threads(void)
+{
+	int i, ran = 0;
+
+	for (i = 0; i < g_nthreads; i++) {
+		ran += stub_poll_thread(i);
+	}
+	return ran;
+}
+
+static bool
+poll_until(volatile int *done, double seconds, bool all_threads)
 {
 	struct timespec t0, t;
 
 	clock_gettime(CLOCK_MONOTONIC, &t0);
 	while (!*done) {
-		stub_poll();
+		if (all_threads) {
+			stub_poll_threads();
+		} else {
+			stub_poll();
+		}
 		clock_gettime(CLOCK_MONOTONIC, &t);
 		if ((t.tv_sec - t0.tv_sec) + (t.tv_nsec - t0.tv_nsec) * 1e-9 > seconds) {
 			return false;
@@ -966,3 +1259,6 @@ stub_poll_until(volatile int *done, double seconds)
 	}
 	return true;
 }
+
+bool stub_poll_until(volatile int *done, double seconds) { return poll_until(done, seconds, true); }
+bool stub_poll_self_until(volatile int *done, double seconds) { return poll_until(done, seconds, false); }

@@ -1,6 +1,6 @@
 /*
- * spdk_stub.h -- test-side controls of the single-threaded SPDK runtime stand-in
- * (spdk_stub.c) that the raid module harnesses link instead of libspdk.
+ * spdk_stub.h -- test-side controls of the SPDK runtime stand-in (spdk_stub.c)
+ * that the raid module harnesses link instead of libspdk.
  */
 #ifndef DRAID_TEST_SPDK_STUB_H
 #define DRAID_TEST_SPDK_STUB_H
@@ -18,8 +18,12 @@ void stub_inject_io_error(struct spdk_bdev *bdev, int count);
 void stub_inject_enomem(struct spdk_bdev *bdev, int count);
 /* Every I/O of the bdev fails from now on (a dead disk) / works again. */
 void stub_set_dead(struct spdk_bdev *bdev, bool dead);
-/* Delivers SPDK_BDEV_EVENT_REMOVE to every open descriptor of the bdev. */
+/* Sends SPDK_BDEV_EVENT_REMOVE to every open descriptor of the bdev, each as a
+ * message on the thread that opened it (delivered by that thread's next poll). */
 void stub_hot_remove(struct spdk_bdev *bdev);
+/* Reads and writes of the bdev complete without moving data, as on
+ * module/bdev/null: what is left to measure is the code above the base bdevs. */
+void stub_set_null_io(struct spdk_bdev *bdev, bool null_io);
 
 struct stub_bdev_stats {
 	uint64_t reads, writes, read_blocks, write_blocks, enomem, failed;
@@ -37,11 +41,42 @@ int stub_bdev_submit(struct spdk_bdev *bdev, struct spdk_io_channel *ch, enum sp
 
 struct spdk_bdev *stub_bdev_by_name(const char *name);
 
-/* One reactor iteration: messages, io_wait retries, base bdev completions,
- * pollers.  Returns the number of things that ran. */
+/* SPDK threads, in the manner of test/common/lib/ut_multithread.c
+ * (allocate_threads / set_thread / poll_thread / poll_threads).  One thread
+ * (id 0) exists from the start.  stub_set_thread() makes a thread current for
+ * the calling OS thread: spdk_get_thread() returns it, channels, pollers and
+ * descriptors created from then on belong to it.  One OS thread can step all
+ * of them (deterministic interleaving), or each can be driven by an OS thread of
+ * its own that calls stub_set_thread(id) once and then stub_poll(). */
+#define STUB_MAX_THREADS 16
+int stub_allocate_threads(int num_threads);
+int stub_num_threads(void);
+void stub_set_thread(int id);
+int stub_thread_id(const struct spdk_thread *thread);
+
+struct stub_thread_stats {
+	uint64_t msgs;				/* messages sent to the thread */
+	uint64_t msgs_from_other_threads;	/* ... by a thread other than itself */
+};
+void stub_thread_stats(int id, struct stub_thread_stats *out, bool reset);
+
+/* One reactor iteration of the current thread: messages, io_wait retries, base
+ * bdev completions, pollers.  Returns the number of things that ran. */
 int stub_poll(void);
-/* Polls until `*done` is non-zero; false on time-out (seconds). */
+/* One iteration of thread `id` / of every thread in turn, from one OS thread. */
+int stub_poll_thread(int id);
+int stub_poll_threads(void);
+/* Polls every thread in turn until `*done` is non-zero; false on time-out (seconds). */
 bool stub_poll_until(volatile int *done, double seconds);
+/* The same, polling only the current thread (for a thread run by its own OS thread). */
+bool stub_poll_self_until(volatile int *done, double seconds);
+
+/* What the runtime still holds: spdk_bdev_io's not yet freed, open descriptors,
+ * io_channels, pollers, undelivered messages, DMA blocks, io_devices. */
+struct stub_live {
+	int64_t ios, descs, channels, pollers, msgs, dma, io_devices;
+};
+void stub_live(struct stub_live *out);
 
 /* 0 errors only (default), 1 + warnings, 2 + notices, 3 everything. */
 void stub_set_log_level(int level);

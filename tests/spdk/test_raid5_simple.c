@@ -51,7 +51,7 @@ io_done(struct spdk_bdev_io *bdev_io, bool success, void *cb_arg)
 
 	w->success = success;
 	w->done = 1;
-	free(bdev_io);
+	spdk_bdev_free_io(bdev_io);
 }
 
 static bool

@@ -487,3 +487,94 @@ def test_sg_back_to_back_flushes(ec):
         ctx.close()
     got = reverse_strip(buf.cpu().numpy())
     assert (got == oracle_encode_np(got, k, m)).all()
+
+
+def test_sg_fence_orders_a_request_behind_its_own_rebuild(ec):
+    """Several requests share one batch.  Request A opens the encode group; request B
+    (a degraded partial write, raid5.c:743-777 with a lost strip) then queues the rebuild
+    of a lost data strip and, behind a fence, an encode that reads the rebuilt strip.
+    Groups launch in the order of their first segment, so without the fence B's encode
+    would ride with A's, ahead of B's rebuild.  Many B's and A's interleaved; every
+    parity must equal the oracle's over the true data."""
+    k, m, L, B = 8, 2, 16384, 24
+    n = k + m
+    g = torch.Generator(device=DEV)
+    g.manual_seed(77)
+    buf = torch.randint(0, 256, (B, n, L), dtype=torch.uint8, device=DEV, generator=g)
+    ref = buf.cpu().numpy()
+    ref[:, k:] = 0
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, B, L, n * L) == 0
+    buf.copy_(torch.from_numpy(ref))           # consistent stripes
+    lost = [(3 * s + 1) % k for s in range(B)]
+    out = torch.full((B, m, L), 0xEE, dtype=torch.uint8, device=DEV)   # fresh parity per stripe
+    for s in range(B):
+        if s % 3:                               # B-type stripes: the lost strip starts as garbage
+            buf[s, lost[s]] = 0x5A
+    base, obase = buf.data_ptr(), out.data_ptr()
+    torch.cuda.synchronize()
+
+    def strips(s, parity_base):
+        rows = [[(base + (s * n + j) * L, L)] for j in range(k)]
+        return rows + [[(parity_base(j), L)] for j in range(m)]
+
+    ctx = ec.Ctx()
+    try:
+        for s in range(B):
+            ctx.mark()
+            if s % 3 == 0:                      # request A: a plain encode
+                ctx.encode_sg(k, m, strips(s, lambda j: obase + (s * m + j) * L), L)
+                continue
+            # request B: rebuild the lost strip from P and Q ...
+            ctx.reconstruct_sg(k, m, strips(s, lambda j: base + (s * n + k + j) * L), L,
+                               [lost[s]])
+            ctx.fence()
+            # ... then re-encode over it into fresh parity buffers
+            ctx.encode_sg(k, m, strips(s, lambda j: obase + (s * m + j) * L), L)
+        ctx.flush()
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    assert (buf.cpu().numpy() == ref).all(), "rebuilt strips"
+    assert (out.cpu().numpy() == ref[:, k:]).all(), "parity encoded behind the fence"
+
+
+def test_sg_mark_and_rollback_drop_exactly_one_request(ec):
+    """draid_ec_ctx_mark / rollback: a request whose later queueing call fails leaves
+    nothing queued (its buffers are reused by the next owner), earlier requests stay."""
+    k, m, L = 4, 2, 4096
+    n = k + m
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    buf = torch.randint(0, 256, (3, n, L), dtype=torch.uint8, device=DEV, generator=g)
+    buf[:, k:] = 0x11
+    before = buf.cpu().numpy()
+    base = buf.data_ptr()
+    torch.cuda.synchronize()
+
+    def strips(s):
+        return [[(base + (s * n + j) * L, L)] for j in range(n)]
+
+    ctx = ec.Ctx()
+    try:
+        assert ec.lib().draid_ec_ctx_rollback(ctx.h) == 1      # no mark yet
+        ctx.encode_sg(k, m, strips(0), L)                       # request 0 stays
+        ctx.mark()
+        ctx.reconstruct_sg(k, m, strips(1), L, [0, 2])          # request 1: two groups ...
+        ctx.fence()
+        ctx.encode_sg(k, m, strips(1), L)
+        assert ctx.queued() == 3
+        ctx.rollback()                                          # ... all dropped
+        assert ctx.queued() == 1
+        ctx.mark()
+        ctx.encode_sg(k, m, strips(2), L)                       # request 2 queues normally
+        ctx.flush()
+        assert ec.lib().draid_ec_ctx_rollback(ctx.h) == 1      # launched: cannot be undone
+        ctx.synchronize()
+    finally:
+        ctx.close()
+    got = buf.cpu().numpy()
+    ref = before.copy()
+    ref[:, k:] = 0
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, 3, L, n * L) == 0
+    assert (got[0] == ref[0]).all() and (got[2] == ref[2]).all()
+    assert (got[1] == before[1]).all(), "the rolled-back request touched its buffers"

@@ -1,10 +1,16 @@
-"""The engine under the reference's own code, three ways (binaries under oracle/_ref/,
-built by tests/spdk/Makefile from reference sources where they lie):
+"""The engine under the reference's own code (binaries under tests/spdk/build/, built by
+tests/spdk/Makefile from reference sources where they lie):
 
 * spdk_raid_module_test -- draid-spdk_amd/spdk/raid_gpu.c (a `struct raid_bdev_module`
   for RAID6, and RAID5) linked with the reference's bdev_raid.c: full-stripe, partial and
   degraded I/O through raid_bdev_submit_request, completed from the module's poller, every
   disk byte checked against the oracle, disks failed through base_info->degraded;
+* spdk_raid_threads_test -- the same module on four SPDK threads with one channel each:
+  requests from all of them interleaved on the same stripes (stepped from one OS thread,
+  then with one OS thread per SPDK thread), cross-thread hand-off of a stripe observed, a
+  base bdev hot-removed under I/O (the reference's behaviour: the array goes offline);
+* spdk_raid_hotremove_test -- the hot-remove with the documented one-statement redirect
+  compiled into the reference's framework: the array stays online, degraded;
 * spdk_raid5_simple_test -- the reference's raid5_simple.c, unmodified, calling xor_gen at
   its own call site with the engine behind it, on raid5_ut_ref.c's known-answer flow;
 * gf_vect_mul_ref -- the reference's P+Q example, unmodified, with its own self-checks.
@@ -19,8 +25,9 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
-OUT = os.path.join(ROOT, "oracle", "_ref")
-BINARIES = ("spdk_raid_module_test", "spdk_raid5_simple_test", "gf_vect_mul_ref")
+OUT = os.path.join(ROOT, "tests", "spdk", "build")
+BINARIES = ("spdk_raid_module_test", "spdk_raid5_simple_test", "gf_vect_mul_ref",
+            "spdk_raid_threads_test", "spdk_raid_hotremove_test", "spdk_raid_module_bench")
 
 
 def build():
@@ -47,6 +54,11 @@ def test_module_compiles_against_the_reference_headers_and_links_with_its_framew
     # the module's parity arithmetic is the C ABI, nothing else
     assert "draid_ec_ctx_flush_ticket" in undefined and "draid_raid_stripe_write" in undefined
     assert "orc_" not in undefined and "xor_gen" not in undefined
+    # the redirect is in the second framework object and only there
+    for obj, want in (("bdev_raid_ref.o", False), ("bdev_raid_hotremove.o", True)):
+        u = subprocess.run(["nm", "-u", os.path.join(OUT, obj)], capture_output=True, text=True,
+                           check=True).stdout
+        assert ("raid_gpu_base_bdev_removed" in u) == want, obj
     # the shim exports isa-l's names
     shim = subprocess.run(["nm", "-D", os.path.join(ROOT, "draid-spdk_amd", "libdraid_isal.so")],
                           capture_output=True, text=True, check=True).stdout
@@ -80,6 +92,27 @@ def test_raid6_module_routes_stripes_over_several_device_slots():
     polled by the channel's poller.  The same array checks must pass."""
     out = run("spdk_raid_module_test", env={"DRAID_RAID_GPUS": "3"})
     assert "ok raid6 n=10 strip=64KiB" in out and "array checks passed" in out
+
+
+@pytest.mark.gpu
+def test_module_on_four_spdk_threads_and_through_hot_remove():
+    """raid5.c:496-505,1047-1054: requests of one stripe run one at a time, in arrival
+    order, and a finished request hands the stripe to the next one's thread.  Four channels
+    on four SPDK threads hit the same stripes; every read must see the writes submitted
+    before it, every disk byte must match the oracle, and at least one hand-off must cross
+    threads.  Then a base bdev is removed under I/O (bdev_raid.c:1333-1390)."""
+    out = run("spdk_raid_threads_test")
+    assert "ok interleaved: 4 SPDK threads" in out
+    assert out.count("ok OS threads: 4 pthreads") == 2
+    assert "ok hot-remove, reference behaviour: array offline" in out
+    hand = [ln for ln in out.splitlines() if "interleaved:" in ln and "hand-offs" in ln]
+    assert hand and int(hand[0].split("hand-offs")[1].split(",")[0]) > 0, hand
+
+
+@pytest.mark.gpu
+def test_hot_remove_with_the_redirect_keeps_the_array_online():
+    out = run("spdk_raid_hotremove_test")
+    assert "ok hot-remove with the redirect: online through two removals, offline at the third" in out
 
 
 @pytest.mark.gpu
