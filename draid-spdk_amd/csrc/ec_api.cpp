@@ -15,6 +15,7 @@
 #include "../../include/draid_ec.h"
 #include "ec_gf.hpp"
 #include "ec_launch.hpp"
+#include "per_device.hpp"
 
 using draid::ArgPtrTable;
 using draid::kMaxArgPtrs;
@@ -48,9 +49,11 @@ namespace {
 
 hipStream_t sync_stream() { return hipStreamPerThread; }
 
-// Per-thread device scratch: a pointer table for calls with more vectors than
-// fit in kernel arguments, a 4-byte flag for the *_check calls, and a staging
-// arena for vectors in pageable host memory.
+// Per-thread, per-GPU device scratch: a pointer table for calls with more
+// vectors than fit in kernel arguments, a 4-byte flag for the *_check calls, and
+// a staging arena for vectors in pageable host memory.  Each is memory of the
+// GPU that was current when it was allocated, so a thread that moves to another
+// GPU (draid_ec_set_device) gets that GPU's own set.
 struct Scratch {
     void* table = nullptr;
     size_t table_bytes = 0;
@@ -67,7 +70,23 @@ struct Scratch {
             (void)hipFree(arena);
     }
 };
-thread_local Scratch t_scratch;
+thread_local draid::PerDevice<Scratch> t_scratch_of;
+
+// The calling thread's scratch on its current GPU; null (with the error
+// recorded) when there is no usable current device.
+Scratch* scratch()
+{
+    int dev = -1;
+    const hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) {
+        (void)fail_hip(e, "hipGetDevice");
+        return nullptr;
+    }
+    Scratch* s = t_scratch_of.at(dev);
+    if (!s)
+        (void)fail_arg("the current GPU's ordinal is beyond what the library keeps state for");
+    return s;
+}
 
 // The vectors of one synchronous call as a kernel may address them.
 //
@@ -91,6 +110,7 @@ struct Vectors {
     };
     std::vector<Staged> staged;
     size_t len = 0;
+    uint8_t* arena = nullptr;  // the staging arena the offsets refer to (this call's GPU)
 
     int resolve(void* const* host, const uint8_t* use, int n, size_t bytes)
     {
@@ -101,12 +121,15 @@ struct Vectors {
         std::vector<int> slot(static_cast<size_t>(n), -1);
         for (int i = 0; i < n; ++i) {
             const void* d = nullptr;
-            if (draid::translate(host[i], bytes, &d) == 0) {
+            const int how = draid::translate(host[i], bytes, &d);
+            if (how == 0) {
                 dev[i] = const_cast<void*>(d);
                 continue;
             }
             if (!host[i])
                 return fail_arg("a vector pointer is NULL");
+            if (how == 2)
+                return fail_arg("a vector is device memory of a GPU other than the current one");
             for (size_t s = 0; s < staged.size(); ++s)
                 if (staged[s].host == host[i])
                     slot[i] = static_cast<int>(s);
@@ -117,25 +140,30 @@ struct Vectors {
             }
             staged[slot[i]].use |= use[i];
         }
+        arena = nullptr;
         if (staged.empty())
             return 0;
-        if (t_scratch.arena_bytes < need) {
-            if (t_scratch.arena)
-                (void)hipFree(t_scratch.arena);
-            t_scratch.arena = nullptr;
-            t_scratch.arena_bytes = 0;
-            const hipError_t e = hipMalloc(&t_scratch.arena, need);
+        Scratch* sc = scratch();
+        if (!sc)
+            return -1;
+        if (sc->arena_bytes < need) {
+            if (sc->arena)
+                (void)hipFree(sc->arena);
+            sc->arena = nullptr;
+            sc->arena_bytes = 0;
+            const hipError_t e = hipMalloc(&sc->arena, need);
             if (e != hipSuccess)
                 return fail_hip(e, "hipMalloc(staging for pageable vectors)");
-            t_scratch.arena_bytes = need;
+            sc->arena_bytes = need;
         }
+        arena = sc->arena;
         for (int i = 0; i < n; ++i)
             if (slot[i] >= 0)
-                dev[i] = t_scratch.arena + staged[slot[i]].offset;
+                dev[i] = arena + staged[slot[i]].offset;
         for (const Staged& s : staged) {
             if (!(s.use & kIn))
                 continue;
-            const hipError_t e = hipMemcpyAsync(t_scratch.arena + s.offset, s.host, bytes,
+            const hipError_t e = hipMemcpyAsync(arena + s.offset, s.host, bytes,
                                                 hipMemcpyHostToDevice, sync_stream());
             if (e != hipSuccess)
                 return fail_hip(e, "hipMemcpyAsync(stage pageable vector in)");
@@ -149,7 +177,7 @@ struct Vectors {
         for (const Staged& s : staged) {
             if (!(s.use & kOut))
                 continue;
-            const hipError_t e = hipMemcpyAsync(s.host, t_scratch.arena + s.offset, len,
+            const hipError_t e = hipMemcpyAsync(s.host, arena + s.offset, len,
                                                 hipMemcpyDeviceToHost, sync_stream());
             if (e != hipSuccess)
                 return e;
@@ -186,21 +214,23 @@ int stage_pointers(void* const* array, int n, ArgPtrTable* args, const uint8_t* 
         return 0;
     }
     const size_t bytes = sizeof(void*) * static_cast<size_t>(n);
-    if (t_scratch.table_bytes < bytes) {
-        if (t_scratch.table)
-            (void)hipFree(t_scratch.table);
-        t_scratch.table = nullptr;
-        t_scratch.table_bytes = 0;
-        hipError_t e = hipMalloc(&t_scratch.table, bytes);
+    Scratch* sc = scratch();
+    if (!sc)
+        return -1;
+    if (sc->table_bytes < bytes) {
+        if (sc->table)
+            (void)hipFree(sc->table);
+        sc->table = nullptr;
+        sc->table_bytes = 0;
+        hipError_t e = hipMalloc(&sc->table, bytes);
         if (e != hipSuccess)
             return fail_hip(e, "hipMalloc(pointer table)");
-        t_scratch.table_bytes = bytes;
+        sc->table_bytes = bytes;
     }
-    hipError_t e = hipMemcpyAsync(t_scratch.table, array, bytes, hipMemcpyHostToDevice,
-                                  sync_stream());
+    hipError_t e = hipMemcpyAsync(sc->table, array, bytes, hipMemcpyHostToDevice, sync_stream());
     if (e != hipSuccess)
         return fail_hip(e, "hipMemcpyAsync(pointer table)");
-    *table = static_cast<const uint8_t* const*>(t_scratch.table);
+    *table = static_cast<const uint8_t* const*>(sc->table);
     return 0;
 }
 
@@ -235,8 +265,11 @@ int encode_one(uint32_t k, uint32_t m, int len, void** array)
 
 int check_one(uint32_t k, uint32_t m, int len, void** array)
 {
-    if (!t_scratch.flag) {
-        hipError_t e = hipMalloc(&t_scratch.flag, sizeof(uint32_t));
+    Scratch* sc = scratch();
+    if (!sc)
+        return -1;
+    if (!sc->flag) {
+        hipError_t e = hipMalloc(&sc->flag, sizeof(uint32_t));
         if (e != hipSuccess)
             return fail_hip(e, "hipMalloc(flag)");
     }
@@ -248,15 +281,15 @@ int check_one(uint32_t k, uint32_t m, int len, void** array)
     rc = stage_pointers(t_vec.dev.data(), static_cast<int>(k + m), &args, &table);
     if (rc)
         return rc;
-    hipError_t e = hipMemsetAsync(t_scratch.flag, 0, sizeof(uint32_t), sync_stream());
+    hipError_t e = hipMemsetAsync(sc->flag, 0, sizeof(uint32_t), sync_stream());
     if (e != hipSuccess)
         return fail_hip(e, "hipMemsetAsync(flag)");
     e = draid::launch_check(k, m, static_cast<uint64_t>(len), table, table ? nullptr : &args,
-                            t_scratch.flag, sync_stream());
+                            sc->flag, sync_stream());
     if (e != hipSuccess)
         return fail_hip(e, "launch_check");
     uint32_t host_flag = 0;
-    e = hipMemcpyAsync(&host_flag, t_scratch.flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+    e = hipMemcpyAsync(&host_flag, sc->flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
                        sync_stream());
     rc = finish_sync(e, "hipMemcpyAsync(flag)");
     if (rc)

@@ -261,15 +261,16 @@ struct IovIter {
     intptr_t delta;    // device address = p + delta (0 unless the ctx resolves host pointers)
     bool xl;           // resolve each iovec (draid_ec_ctx_set_host_pointers)
     bool bad;          // an iovec was not GPU accessible
+    int device;        // the context's GPU: where the kernels will run
 
     // Device-address offset of one iovec, or false when the GPU cannot reach it.
-    static bool resolve(const struct iovec& e, intptr_t* d)
+    static bool resolve(const struct iovec& e, intptr_t* d, int device)
     {
         *d = 0;
         if (e.iov_len == 0)
             return true;
         const void* dev = nullptr;
-        if (draid::translate(e.iov_base, e.iov_len, &dev))
+        if (draid::translate(e.iov_base, e.iov_len, &dev, device))
             return false;
         *d = static_cast<const uint8_t*>(dev) - static_cast<const uint8_t*>(e.iov_base);
         return true;
@@ -280,7 +281,7 @@ struct IovIter {
         idx = i;
         p = static_cast<const uint8_t*>(v[i].iov_base);
         left = v[i].iov_len;
-        if (xl && !resolve(v[i], &delta))
+        if (xl && !resolve(v[i], &delta, device))
             bad = true;
     }
 };
@@ -316,12 +317,12 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     for (uint32_t j = 0; j < n; ++j) {
         if (!iovs || !iovs[j] || !iovcnt || iovcnt[j] < 0)
             return ctx_arg("iovec list missing");
-        it[j] = IovIter{iovs[j], iovcnt[j], 0, nullptr, 0, 0, c->host_pointers, false};
+        it[j] = IovIter{iovs[j], iovcnt[j], 0, nullptr, 0, 0, c->host_pointers, false, c->device};
         if (len && !iter_seek(it[j], offset ? offset[j] : 0))
             return ctx_arg("iovec list shorter than offset");
         if (it[j].bad)
-            return ctx_arg("an iovec is neither device memory nor pinned / registered host "
-                           "memory");
+            return ctx_arg("an iovec is neither memory of the context's GPU nor pinned / "
+                           "registered host memory");
     }
     Group& g = group_for(c, op, k, m);
     if (const int rc = g.ready())
@@ -362,7 +363,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                     break;
                 if (t.xl) {  // adjacent for the host: also adjacent for the device?
                     intptr_t d;
-                    if (!IovIter::resolve(t.v[x], &d) || d != t.delta)
+                    if (!IovIter::resolve(t.v[x], &d, t.device) || d != t.delta)
                         break;
                 }
                 avail += t.v[x].iov_len;
@@ -372,8 +373,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
         }
         for (uint32_t j = 0; j < n; ++j)
             if (it[j].bad)
-                return rollback("an iovec is neither device memory nor pinned / registered host "
-                                "memory");
+                return rollback("an iovec is neither memory of the context's GPU nor pinned / "
+                                "registered host memory");
         if (g.len.empty())
             g.first_seq = c->seq;
         ++c->seq;

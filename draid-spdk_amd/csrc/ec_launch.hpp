@@ -90,10 +90,14 @@ int fail_arg(const char* what);
 
 // Pointer resolution (ec_xlate.cpp): the address a kernel may use for the
 // caller's [p, p + len) -- device memory as is, pinned / registered host memory
-// at its device address.  Returns 0, or 1 when the range is not GPU accessible
-// (pageable host memory): such a pointer must never reach a kernel.  Results are
-// cached per thread; translate_invalidate() empties every thread's cache.
-int translate(const void* p, size_t len, const void** dev);
+// at its device address.  Returns 0; 1 when the range is not GPU accessible
+// (pageable host memory: stage it or reject it); 2 when it is device memory of a
+// GPU other than `on_device` (reject it).  Neither may ever reach a kernel.  on_device is the ordinal of the GPU
+// the kernel will run on; kCurrentDevice = the calling thread's current one.
+// Results are cached per thread; translate_invalidate() empties every thread's
+// cache.
+constexpr int kCurrentDevice = -2;
+int translate(const void* p, size_t len, const void** dev, int on_device = kCurrentDevice);
 void translate_invalidate();
 
 // Variant selector for A/B experiments inside one process (0 = default).

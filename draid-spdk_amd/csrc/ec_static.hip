@@ -13,6 +13,13 @@
 // device-accessible word instead of copying it back: no hipMalloc, hipFree,
 // hipMemcpy or synchronisation anywhere on the path.
 //
+// Like every pointer-taking entry point it resolves the vectors and the result
+// word before any kernel sees them (ec_xlate.cpp: a cached lookup per pointer,
+// no allocation): device memory of the current GPU and pinned / registered host
+// memory are used at their device addresses; anything else -- pageable memory,
+// which draid_pq_check() would stage through an arena this variant must not
+// allocate -- is an error return with nothing launched, never a GPU fault.
+//
 // The array is shared by every call on a GPU: calls that overlap on one GPU
 // (different streams or threads) race on it.
 #include <hip/hip_runtime.h>
@@ -94,6 +101,20 @@ extern "C" int draid_pq_check_static(int vects, int len, void** array, uint32_t*
                                "vectors do not fit the static pointer table");
     if (!draid::launch_fits(static_cast<uint64_t>(len), 1))
         return draid::fail_arg("pq_check_static: len above 0x7fff0000");
+    // every address first: nothing is launched unless the GPU can reach all of them
+    const uint8_t* vec[kStaticMaxVects];
+    for (int i = 0; i < vects; ++i) {
+        const void* d = nullptr;
+        if (len > 0 && draid::translate(array[i], static_cast<size_t>(len), &d))
+            return draid::fail_arg("pq_check_static: a vector is neither memory of the current GPU "
+                                   "nor pinned / registered host memory (pageable vectors need "
+                                   "draid_pq_check, which may allocate a staging arena)");
+        vec[i] = static_cast<const uint8_t*>(d);
+    }
+    const void* res = nullptr;
+    if (draid::translate(result, sizeof(uint32_t), &res))
+        return draid::fail_arg("pq_check_static: the result word is neither memory of the current "
+                               "GPU nor pinned / registered host memory");
     unsigned char* scr = nullptr;
     if (const int rc = scratch_of(&scr))
         return rc;
@@ -104,7 +125,7 @@ extern "C" int draid_pq_check_static(int vects, int len, void** array, uint32_t*
         PtrChunk c{};
         const int n = vects - off < kChunkPtrs ? vects - off : kChunkPtrs;
         for (int i = 0; i < n; ++i)
-            c.p[i] = static_cast<const uint8_t*>(array[off + i]);
+            c.p[i] = vec[off + i];
         hipLaunchKernelGGL(k_static_stage, dim3(1), dim3(64), 0, st, table, flag, c, off, n,
                            off == 0);
         const hipError_t e = hipGetLastError();
@@ -117,7 +138,8 @@ extern "C" int draid_pq_check_static(int vects, int len, void** array, uint32_t*
                                 table, nullptr, flag, st);
     if (e != hipSuccess)
         return draid::fail_hip(e, "launch_check");
-    hipLaunchKernelGGL(k_static_finish, dim3(1), dim3(1), 0, st, flag, result);
+    hipLaunchKernelGGL(k_static_finish, dim3(1), dim3(1), 0, st, flag,
+                       static_cast<uint32_t*>(const_cast<void*>(res)));
     e = hipGetLastError();
     return e == hipSuccess ? 0 : draid::fail_hip(e, "launch(k_static_finish)");
 }

@@ -13,6 +13,10 @@
 //   anything else                   -> "not accessible" (the caller stages or
 //                                      rejects it; it is never handed to a kernel)
 //
+// Device memory belongs to one GPU: a range resolved there is good for kernels
+// on that GPU only (no peer access is set up by this library), so every range
+// remembers its device and a lookup says which GPU the kernel will run on.
+//
 // hipPointerGetAttributes costs microseconds, so each thread keeps the ranges it
 // has resolved (the whole allocation or registration around the pointer) and a
 // hit costs a few compares.  Ranges go stale when memory is freed or
@@ -26,12 +30,14 @@
 
 #include "../../include/draid_ec.h"
 #include "ec_launch.hpp"
+#include "per_device.hpp"
 
 namespace {
 
 struct Range {
     uintptr_t lo = 0, hi = 0;  // host-side name of the range: [lo, hi)
     intptr_t delta = 0;        // device address = host address + delta
+    int device = draid::kAnyDevice;  // the GPU whose memory it is; host memory: any
 };
 
 constexpr int kWays = 32;
@@ -55,9 +61,11 @@ int query(const void* p, size_t len, Range* out)
     }
     const uintptr_t q = reinterpret_cast<uintptr_t>(p);
     uintptr_t dev = 0;
-    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
-        a.type == hipMemoryTypeUnified) {
+    if (a.type == hipMemoryTypeDevice) {
         dev = q;
+        out->device = a.device;
+    } else if (a.type == hipMemoryTypeManaged || a.type == hipMemoryTypeUnified) {
+        dev = q;  // migrates to whichever GPU touches it
     } else if (a.type == hipMemoryTypeHost && a.devicePointer) {
         // devicePointer names the same byte as hostPointer, which is p itself or
         // the start of its mapping depending on the runtime version
@@ -113,7 +121,25 @@ int query(const void* p, size_t len, Range* out)
 
 namespace draid {
 
-int translate(const void* p, size_t len, const void** dev)
+// The GPU a kernel launched now would run on.
+static int current_device()
+{
+    int d = kAnyDevice;
+    if (hipGetDevice(&d) != hipSuccess) {
+        (void)hipGetLastError();
+        return kAnyDevice;
+    }
+    return d;
+}
+
+static bool usable(const Range& r, int on_device)
+{
+    if (r.device == kAnyDevice || on_device == kAnyDevice)
+        return true;
+    return range_usable_on(r.device, on_device == kCurrentDevice ? current_device() : on_device);
+}
+
+int translate(const void* p, size_t len, const void** dev, int on_device)
 {
     *dev = nullptr;
     if (!p)
@@ -132,6 +158,8 @@ int translate(const void* p, size_t len, const void** dev)
             for (int j = i; j > 0; --j)  // move to front
                 c.r[j] = c.r[j - 1];
             c.r[0] = hit;
+            if (!usable(hit, on_device))
+                return 2;  // another GPU's memory
             *dev = reinterpret_cast<const void*>(q + static_cast<uintptr_t>(hit.delta));
             return 0;
         }
@@ -144,6 +172,8 @@ int translate(const void* p, size_t len, const void** dev)
     for (int j = c.n - 1; j > 0; --j)
         c.r[j] = c.r[j - 1];
     c.r[0] = r;
+    if (!usable(r, on_device))
+        return 2;
     *dev = reinterpret_cast<const void*>(q + static_cast<uintptr_t>(r.delta));
     return 0;
 }
@@ -161,8 +191,8 @@ int draid_ec_device_pointer(const void* ptr, size_t len, void** dev_ptr)
     const void* d = nullptr;
     if (draid::translate(ptr, len, &d)) {
         *dev_ptr = nullptr;
-        return draid::fail_arg("device_pointer: the range is not device memory and not pinned or "
-                               "registered host memory");
+        return draid::fail_arg("device_pointer: the range is not memory of the current GPU and "
+                               "not pinned or registered host memory");
     }
     *dev_ptr = const_cast<void*>(d);
     return 0;

@@ -76,14 +76,22 @@ int draid_pq_check(int vects, int len, void **array);
  * table in device memory it allocates on first use; this variant keeps both in
  * a 4 KiB static device array inside the library (one copy per GPU, held until
  * the process ends) and allocates, frees and copies nothing.
- * Same arguments and argument errors as draid_pq_check(), plus:
+ * Same arguments and argument errors as draid_pq_check(), except:
+ *   array  every vector must be memory the GPU can use in place -- device memory
+ *          of the current GPU, or pinned / registered host memory (host or device
+ *          address) -- because a pageable vector would need the staging arena
+ *          draid_pq_check() allocates: such a vector returns 1 and nothing is
+ *          launched (it is never handed to a kernel);
  *   vects  at most DRAID_PQ_CHECK_STATIC_MAX_VECTS (the static table), else 1;
- *   result device-accessible word (device memory, or the device address of
- *          pinned / registered host memory); receives 0 if P and Q match, 1 if not;
+ *   result word of the same kinds of memory; receives 0 if P and Q match, 1 if not;
  *   stream the work is enqueued here and the call returns without waiting:
  *          *result is valid once the stream has finished.
  * Every call on a GPU shares that GPU's array: calls that overlap in time on
- * one GPU (other streams or threads) race and may report the wrong verdict. */
+ * one GPU (other streams or threads) race and may report the wrong verdict.
+ * Under stream capture: a thread's first call on a GPU looks the array's address
+ * up (hipGetSymbolAddress) and its first call with a given buffer asks the
+ * runtime what that memory is; make one call outside the captured region first,
+ * after which a call with the same buffers only launches kernels. */
 #define DRAID_PQ_CHECK_STATIC_MAX_VECTS 257 /* k = 255 data strips + P + Q */
 int draid_pq_check_static(int vects, int len, void **array, uint32_t *result, void *stream);
 

@@ -24,6 +24,18 @@ def test_c_harness_host_logic():
     assert "PASS" in out.stdout
 
 
+def test_per_device_state_keying():
+    """State that lives in one GPU's memory is kept per GPU (csrc/per_device.hpp): a
+    thread that moves from GPU 0 to GPU 1 never gets GPU 0's scratch, and a device
+    address is only vouched for on the GPU that owns it.  Pure host logic, under
+    ASan + UBSan."""
+    _build()
+    out = subprocess.run([os.path.join(HERE, "c", "test_per_device")], capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "PASS" in out.stdout
+
+
 @pytest.mark.gpu
 def test_c_harness_gpu(ec):
     _build()

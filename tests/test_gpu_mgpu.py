@@ -78,3 +78,52 @@ def test_mgpu_argument_errors(ec):
     assert L.draid_ec_mgpu_create(None, 1, None) == 1
     assert L.draid_ec_mgpu_query(None) == 1
     assert L.draid_ec_mgpu_encode(None, None) == 1
+
+
+def test_isal_calls_on_one_thread_across_two_gpus(ec):
+    """The relinked reference calls xor_gen / pq_gen from whichever reactor thread, with
+    whichever GPU that thread last selected (raid5.c:188-201 is the call site).  The calls'
+    per-thread device scratch -- the staging arena for pageable vectors, the pointer table
+    of wide stripes, the check flag -- is memory of ONE GPU, so it is kept per GPU: the
+    same thread runs pq_gen / pq_check / recover on pageable memory on GPU 0, then on
+    GPU 1, then on GPU 0 again, and a GPU 0 device pointer is refused on GPU 1 instead of
+    being handed to a kernel there."""
+    import ctypes as C
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs: one GPU cannot show state of GPU 0 being used on GPU 1")
+    k, L = 40, 8192                      # 42 vectors: beyond kernel arguments -> pointer table
+    rng = np.random.default_rng(11)
+    host = np.zeros((k + 2, L), np.uint8)
+    host[:k] = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    ref = host.copy().reshape(1, k + 2, L)
+    assert oracle.encode_strided(ref.reshape(-1), k, 2, L, 1, L, (k + 2) * L) == 0
+    ptrs = [host[j].ctypes.data for j in range(k + 2)]
+    lib = ec.lib()
+    try:
+        for dev in (0, 1, 0):
+            assert lib.draid_ec_set_device(dev) == 0
+            host[k:] = 0
+            assert ec.pq_gen(ptrs, L) == 0                      # pageable: staged on this GPU
+            assert (host == ref[0]).all(), dev
+            assert ec.pq_check(ptrs, L) == 0
+            host[3] ^= 0xFF
+            assert ec.pq_check(ptrs, L) == 1
+            host[3] = 0
+            host[17] = 0
+            assert ec.recover(k, 2, L, ptrs, [3, 17]) == 0
+            assert (host == ref[0]).all(), dev
+        # device memory of GPU 0 offered to a call running on GPU 1
+        on0 = torch.from_numpy(ref[0]).to("cuda:0")
+        torch.cuda.synchronize(0)
+        d0 = [on0[j].data_ptr() for j in range(k + 2)]
+        assert lib.draid_ec_set_device(1) == 0
+        arr = (C.c_void_p * (k + 2))(*d0)
+        assert lib.draid_pq_check(k + 2, L, arr) == 1
+        assert "other than the current one" in ec.last_error()
+        out = C.c_void_p()
+        assert lib.draid_ec_device_pointer(d0[0], L, C.byref(out)) == 1
+        assert lib.draid_ec_set_device(0) == 0
+        assert ec.pq_check(d0, L) == 0
+        assert lib.draid_ec_device_pointer(d0[0], L, C.byref(out)) == 0 and out.value == d0[0]
+    finally:
+        lib.draid_ec_set_device(0)

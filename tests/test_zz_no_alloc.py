@@ -101,3 +101,46 @@ def test_static_check_widest_and_limits(ec):
         assert L.draid_pq_check_static(10, 1024, arr, None, stream) == 1
     finally:
         ec.stream_destroy(stream)
+
+
+def test_static_check_resolves_its_pointers(ec):
+    """Like every pointer-taking entry point, the static check resolves what it is given
+    before a kernel sees it: a vector or a result word in pageable host memory returns 1
+    and launches nothing (it is never a GPU fault); pinned host memory is used in place,
+    passed by its HOST address."""
+    stream = ec.stream_create()
+    result = torch.zeros(1, dtype=torch.int32, device=DEV)
+    try:
+        k, L = 6, 4096
+        stripe = make_stripe(k, L, 9)
+        ptrs = [stripe[j].data_ptr() for j in range(k + 2)]
+        # a pageable vector: rejected, the result word keeps its value
+        pageable = np.zeros(L, np.uint8)
+        bad = list(ptrs)
+        bad[2] = pageable.ctypes.data
+        result.fill_(7)
+        torch.cuda.synchronize()
+        assert ec.lib().draid_pq_check_static(k + 2, L, (C.c_void_p * (k + 2))(*bad),
+                                              result.data_ptr(), stream) == 1
+        assert "pageable" in ec.last_error()
+        ec.stream_synchronize(stream)
+        torch.cuda.synchronize()
+        assert int(result.item()) == 7
+        # a pageable result word: rejected too
+        word = np.zeros(1, np.uint32)
+        assert ec.lib().draid_pq_check_static(k + 2, L, (C.c_void_p * (k + 2))(*ptrs),
+                                              word.ctypes.data, stream) == 1
+        # pinned host memory by its host address: data strips and the result word
+        host = torch.empty((k + 2, L), dtype=torch.uint8).pin_memory()
+        host.copy_(stripe.cpu())
+        verdict = torch.full((4,), 5, dtype=torch.int32).pin_memory()
+        hptrs = [host[j].data_ptr() for j in range(k + 2)]
+        assert ec.pq_check_static(hptrs, L, verdict.data_ptr(), stream) == 0, ec.last_error()
+        ec.stream_synchronize(stream)
+        assert int(verdict[0]) == 0 and ec.pq_check(hptrs, L) == 0
+        host[k + 1, 100] ^= 2
+        assert ec.pq_check_static(hptrs, L, verdict.data_ptr(), stream) == 0
+        ec.stream_synchronize(stream)
+        assert int(verdict[0]) == 1 and ec.pq_check(hptrs, L) == 1
+    finally:
+        ec.stream_destroy(stream)
