@@ -79,7 +79,7 @@ __device__ __forceinline__ RecPlan decode_failures(int k, uint32_t f0, uint32_t 
     if (M == 1)
         pl.lostQ = false;  // index k + 1 is outside a RAID5 stripe (counted by oob)
     const int nf = pl.nd + (pl.lostP ? 1 : 0) + (pl.lostQ ? 1 : 0);
-    pl.skip = (nf == 0) || (nf > M);
+    pl.skip = (nf == 0) || (nf > M) || oob;  // a counted stripe is left untouched
     pl.bad = oob || nf > M;
     pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
     return pl;
@@ -106,7 +106,7 @@ __device__ __forceinline__ RecPlan decode_failures_mask(uint32_t f0, uint32_t f1
     pl.lostP = (L >> K) & 1u;
     pl.lostQ = M == 2 && ((L >> (K + 1)) & 1u);
     const int nf = __builtin_popcount(L);
-    pl.skip = (nf == 0) || (nf > M);
+    pl.skip = (nf == 0) || (nf > M) || oob;  // a counted stripe is left untouched
     pl.bad = oob || nf > M;
     pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
     return pl;

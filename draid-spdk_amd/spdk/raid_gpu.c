@@ -25,10 +25,12 @@
  *   per-channel resources    raid5_io_channel_resource_init, raid5.c:1491-1541
  *
  * Where the reference calls isa-l synchronously on the reactor, this module
- * queues the stripe's parity work on a per-channel draid_ec_ctx and returns; a
- * poller flushes what the reactor iteration queued as ONE launch and finishes
- * the requests of each flush when its ticket completes.  A reactor never waits
- * for the GPU.
+ * puts a request whose data and prereads are in on its channel's ready list and
+ * returns; the channel's poller walks ready requests onto a per-channel
+ * draid_ec_ctx, launches them together (at most two launches in flight per GPU,
+ * each at most half of the channel's requests: see rg_poll) and finishes the
+ * requests of each launch when its ticket completes.  A reactor never waits for
+ * the GPU.
  *
  * Degraded operation (bdev_raid.h:91-92,163; the reference only has the flags
  * and a commented-out setter, bdev_raid.c:1157-1170): requests read the
@@ -60,8 +62,15 @@
 
 /* Stripe requests in flight per channel (raid5_simple.c:14 keeps 128 with one
  * parity buffer each; here each owns n strip buffers). */
-#define RG_MAX_REQUESTS 64
+#define RG_REQUESTS_DEFAULT 64
+#define RG_REQUESTS_MAX 512
 #define RG_MAX_GPUS 8
+/* Launches a channel keeps in flight per GPU.  While that many run, what the
+ * reactor queues waits for the next poll instead of being launched in ever
+ * smaller pieces: one batch computes while the next one grows, the GPU never
+ * idles for lack of a queued launch, and a flush never has to wait for one of
+ * the context's descriptor ring slots. */
+#define RG_MAX_INFLIGHT 2
 #define RG_CACHE_STRIPES RAID_MAX_STRIPES
 
 enum rg_kind { RG_WRITE_FULL, RG_WRITE_PARTIAL, RG_WRITE_DEGRADED, RG_READ };
@@ -79,6 +88,7 @@ struct rg_info {
 	draid_stripe_cache *stripes;	/* per-stripe request queue, shared by the channels */
 	int ngpus;			/* slots: contexts per channel, stripe s on slot s mod ngpus */
 	int ndevices;			/* GPUs the slots are dealt over */
+	int nrequests;			/* stripe requests (with n strip buffers each) per channel */
 	int refs;			/* the raid bdev (until stop) + every open channel */
 	bool stopped;			/* stop has run: new requests fail, running ones finish */
 	struct raid_gpu_stats stats;
@@ -98,6 +108,43 @@ rg_info_put(struct rg_info *info)
 }
 
 #define RG_COUNT(info, field) __atomic_fetch_add(&(info)->stats.field, 1, __ATOMIC_RELAXED)
+
+/* Section timing for the module bench (raid_gpu.h, struct raid_gpu_prof). */
+#ifdef DRAID_RAID_GPU_PROFILE
+static struct raid_gpu_prof g_prof;
+
+static inline uint64_t
+rg_now_ns(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+#define RG_TIC(t) const uint64_t t = rg_now_ns()
+#define RG_TOC(t, section)                                                                  \
+	do {                                                                               \
+		__atomic_fetch_add(&g_prof.section.ns, rg_now_ns() - (t), __ATOMIC_RELAXED); \
+		__atomic_fetch_add(&g_prof.section.calls, 1, __ATOMIC_RELAXED);            \
+	} while (0)
+#else
+#define RG_TIC(t) do {} while (0)
+#define RG_TOC(t, section) do {} while (0)
+#endif
+
+void
+raid_gpu_get_prof(struct raid_gpu_prof *prof, bool reset)
+{
+#ifdef DRAID_RAID_GPU_PROFILE
+	*prof = g_prof;
+	if (reset) {
+		memset(&g_prof, 0, sizeof(g_prof));
+	}
+#else
+	(void)reset;
+	memset(prof, 0, sizeof(*prof));
+#endif
+}
 
 static const char *
 rg_level_name(const struct raid_bdev *raid_bdev)
@@ -148,13 +195,17 @@ struct rg_request {
 struct rg_channel {
 	struct rg_info *info;
 	draid_ec_ctx *ctx[RG_MAX_GPUS];
+	uint64_t last_ticket[RG_MAX_GPUS];	/* of the latest flush */
+	uint64_t done_ticket[RG_MAX_GPUS];	/* highest ticket seen finished */
 	struct spdk_poller *poller;
 	struct rg_request *requests;
-	uint8_t *pool;			/* RG_MAX_REQUESTS * n strip buffers */
+	uint8_t *pool;			/* nrequests * n strip buffers */
+	struct rg_request **batch;	/* the poller's launch under construction */
 	bool pool_registered;		/* this channel registered the pool with the GPU runtime */
 	TAILQ_HEAD(, rg_request) free_reqs;
-	TAILQ_HEAD(, rg_request) queued;	/* parity work queued on a context, not flushed */
-	TAILQ_HEAD(, rg_request) running;	/* flushed: waiting for the ticket */
+	int busy_reqs;			/* stripe requests not on free_reqs */
+	TAILQ_HEAD(, rg_request) ready;	/* data and prereads in: parity work to be launched */
+	TAILQ_HEAD(, rg_request) running;	/* launched: waiting for the ticket */
 	TAILQ_HEAD(, spdk_bdev_io_wait_entry) waiting;	/* parent I/O waiting for a request */
 };
 
@@ -271,9 +322,11 @@ rg_complete(struct rg_request *req, enum spdk_bdev_io_status status)
 	struct spdk_bdev_io_wait_entry *wqe;
 
 	if (req->stripe) {
+		RG_TIC(t_sq);
 		struct draid_stripe_waiter *next = draid_stripe_complete(info->stripes, req->stripe,
 						   &req->waiter);
 		draid_stripe_put(info->stripes, req->stripe);
+		RG_TOC(t_sq, stripe_queue);
 		req->stripe = NULL;
 		if (next) {
 			struct rg_request *nreq = next->arg;
@@ -288,7 +341,12 @@ rg_complete(struct rg_request *req, enum spdk_bdev_io_status status)
 	}
 	req->raid_io = NULL;
 	TAILQ_INSERT_HEAD(&ch->free_reqs, req, link);
-	raid_bdev_io_complete(raid_io, status);
+	ch->busy_reqs--;
+	{
+		RG_TIC(t_c);
+		raid_bdev_io_complete(raid_io, status);
+		RG_TOC(t_c, complete);
+	}
 	wqe = TAILQ_FIRST(&ch->waiting);
 	if (wqe) {
 		TAILQ_REMOVE(&ch->waiting, wqe, link);
@@ -347,6 +405,7 @@ rg_submit_ios(struct rg_request *req)
 	struct raid_bdev *raid_bdev = ch->info->raid_bdev;
 	struct raid_bdev_io_channel *raid_ch = rg_raid_ch(ch);
 
+	RG_TIC(t_io);
 	req->submitting = true;
 	while (req->next_io < req->nio) {
 		struct draid_base_io *io = &req->ios[req->next_io];
@@ -375,6 +434,7 @@ rg_submit_ios(struct rg_request *req)
 			req->waitq.cb_arg = req;
 			spdk_bdev_queue_io_wait(base_info->bdev, base_ch, &req->waitq);
 			req->submitting = false;
+			RG_TOC(t_io, base_submit);
 			return;
 		}
 		req->next_io++;
@@ -385,6 +445,7 @@ rg_submit_ios(struct rg_request *req)
 		}
 	}
 	req->submitting = false;
+	RG_TOC(t_io, base_submit);
 	if (req->remaining == 0) {
 		rg_phase_done(req);
 	}
@@ -408,11 +469,13 @@ rg_issue(struct rg_request *req, int nio, bool write, enum rg_phase phase)
 
 /* ------------------------------------------------------------ parity work */
 
+/* Everything the request's parity work reads is in memory: the poller walks it
+ * onto the context and launches it with whatever else became ready. */
 static void
-rg_gpu_queued(struct rg_request *req)
+rg_gpu_ready(struct rg_request *req)
 {
 	req->phase = RG_PHASE_GPU;
-	TAILQ_INSERT_TAIL(&req->ch->queued, req, link);
+	TAILQ_INSERT_TAIL(&req->ch->ready, req, link);
 }
 
 /* The parity work of a request finished on the GPU. */
@@ -461,6 +524,7 @@ rg_queue_write(struct rg_request *req)
 	struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(req->raid_io);
 	draid_ec_ctx *ctx = req->ch->ctx[req->gpu];
 	int nw = 0, rc;
+	RG_TIC(t_w);
 
 	draid_ec_ctx_mark(ctx);
 	if (req->kind == RG_WRITE_FULL) {
@@ -499,7 +563,27 @@ rg_queue_write(struct rg_request *req)
 		}
 	}
 	req->nio = nw;
-	rg_gpu_queued(req);
+	RG_TOC(t_w, walk);
+	return 0;
+}
+
+/* The rebuild of a degraded read's lost requested range, straight into the
+ * parent's iovecs. */
+static int
+rg_queue_read_rebuild(struct rg_request *req)
+{
+	struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(req->raid_io);
+	draid_ec_ctx *ctx = req->ch->ctx[req->gpu];
+	int rc;
+	RG_TIC(t_w);
+
+	draid_ec_ctx_mark(ctx);
+	rc = draid_raid_stripe_read_rebuild(&req->geom, ctx, &req->sreq, bdev_io->u.bdev.iovs,
+					    bdev_io->u.bdev.iovcnt, req->chunk_buf);
+	RG_TOC(t_w, walk);
+	if (rc) {
+		return rg_queue_failed(req, ctx, rc, "draid_raid_stripe_read_rebuild");
+	}
 	return 0;
 }
 
@@ -553,25 +637,8 @@ rg_phase_done(struct rg_request *req)
 
 	switch (req->phase) {
 	case RG_PHASE_PREREAD:
-		if (req->kind == RG_READ) {
-			/* the surviving ranges are in: rebuild the lost requested range */
-			struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(req->raid_io);
-			draid_ec_ctx *ctx = req->ch->ctx[req->gpu];
-			int rc;
-
-			draid_ec_ctx_mark(ctx);
-			rc = draid_raid_stripe_read_rebuild(&req->geom, ctx, &req->sreq,
-							    bdev_io->u.bdev.iovs, bdev_io->u.bdev.iovcnt,
-							    req->chunk_buf);
-			if (rc) {
-				rg_queue_failed(req, ctx, rc, "draid_raid_stripe_read_rebuild");
-				rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
-				return;
-			}
-			rg_gpu_queued(req);
-		} else if (rg_queue_write(req) != 0) {
-			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
-		}
+		/* the surviving ranges (read) or the prereads (write) are in */
+		rg_gpu_ready(req);
 		break;
 	case RG_PHASE_READ:
 	case RG_PHASE_WRITE:
@@ -616,8 +683,13 @@ rg_start_request(struct rg_request *req)
 				lost_requested |= 1u << disk;
 			}
 		}
-		rc = draid_raid_stripe_read(&req->geom, NULL, &req->sreq, bdev_io->u.bdev.iovs,
-					    bdev_io->u.bdev.iovcnt, req->chunk_buf, req->ios, &nio);
+		{
+			RG_TIC(t_p);
+			rc = draid_raid_stripe_read(&req->geom, NULL, &req->sreq, bdev_io->u.bdev.iovs,
+						    bdev_io->u.bdev.iovcnt, req->chunk_buf, req->ios,
+						    &nio);
+			RG_TOC(t_p, plan);
+		}
 		if (rc) {
 			rg_queue_error(req, rc, "draid_raid_stripe_read");
 			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
@@ -637,15 +709,17 @@ rg_start_request(struct rg_request *req)
 	if (ndeg == 0 && req->sreq.full_stripe) {
 		req->kind = RG_WRITE_FULL;
 		RG_COUNT(info, full_stripe_writes);
-		if (rg_queue_write(req) != 0) {
-			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
-		}
+		rg_gpu_ready(req);
 		return;
 	}
 	if (ndeg == 0) {
 		req->kind = RG_WRITE_PARTIAL;
-		rc = draid_raid_plan_write(&req->geom, &req->sreq, &req->plan, req->chunk_buf, req->ios,
-					   &nio);
+		{
+			RG_TIC(t_p);
+			rc = draid_raid_plan_write(&req->geom, &req->sreq, &req->plan, req->chunk_buf,
+						   req->ios, &nio);
+			RG_TOC(t_p, plan);
+		}
 		if (rc) {
 			rg_queue_error(req, rc, "draid_raid_plan_write");
 			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
@@ -663,9 +737,7 @@ rg_start_request(struct rg_request *req)
 		/* every data strip is new: encode, then skip the writes to lost disks */
 		req->kind = RG_WRITE_FULL;
 		RG_COUNT(info, full_stripe_writes);
-		if (rg_queue_write(req) != 0) {
-			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
-		}
+		rg_gpu_ready(req);
 		return;
 	}
 	/* partial write to a degraded array: read every surviving strip, rebuild the
@@ -713,16 +785,24 @@ rg_submit_rw_request(struct raid_bdev_io *raid_io)
 		return;
 	}
 
-	req->geom = info->geom;
-	rc = draid_raid_map_request(&req->geom, bdev_io->u.bdev.offset_blocks,
-				    bdev_io->u.bdev.num_blocks, &req->sreq);
+	{
+		RG_TIC(t_m);
+		req->geom = info->geom;
+		rc = draid_raid_map_request(&req->geom, bdev_io->u.bdev.offset_blocks,
+					    bdev_io->u.bdev.num_blocks, &req->sreq);
+		RG_TOC(t_m, map);
+	}
 	if (spdk_unlikely(rc != 0)) {
 		SPDK_ERRLOG("request [%" PRIu64 ", +%" PRIu64 ") does not map onto one stripe\n",
 			    bdev_io->u.bdev.offset_blocks, bdev_io->u.bdev.num_blocks);
 		raid_bdev_io_complete(raid_io, SPDK_BDEV_IO_STATUS_FAILED);
 		return;
 	}
-	req->stripe = draid_stripe_get(info->stripes, req->sreq.stripe_index);
+	{
+		RG_TIC(t_sq);
+		req->stripe = draid_stripe_get(info->stripes, req->sreq.stripe_index);
+		RG_TOC(t_sq, stripe_queue);
+	}
 	if (spdk_unlikely(req->stripe == NULL)) {
 		/* every cached stripe is referenced (raid5.c:1310-1318): retry later */
 		struct spdk_bdev_io_wait_entry *wqe = &raid_io->waitq_entry;
@@ -733,6 +813,7 @@ rg_submit_rw_request(struct raid_bdev_io *raid_io)
 		return;
 	}
 	TAILQ_REMOVE(&ch->free_reqs, req, link);
+	ch->busy_reqs++;
 	req->raid_io = raid_io;
 	req->thread = spdk_get_thread();
 	req->gpu = (int)(req->sreq.stripe_index % (uint64_t)info->ngpus);
@@ -741,79 +822,134 @@ rg_submit_rw_request(struct raid_bdev_io *raid_io)
 	req->waiter.arg = req;
 	/* requests on one stripe run one at a time, in arrival order
 	 * (raid5.c:1047-1054) */
-	if (draid_stripe_enqueue(info->stripes, req->stripe, &req->waiter) == 1) {
+	{
+		RG_TIC(t_sq);
+		rc = draid_stripe_enqueue(info->stripes, req->stripe, &req->waiter);
+		RG_TOC(t_sq, stripe_queue);
+	}
+	if (rc == 1) {
 		rg_start_request(req);
 	}
 }
 
 /* ------------------------------------------------------------ poller */
 
+/* A flush failed: `batch` holds the requests walked onto the context for it. */
 static void
-rg_fail_queued(struct rg_channel *ch, int gpu)
+rg_fail_batch(struct rg_channel *ch, int gpu, struct rg_request **batch, int n)
 {
-	struct rg_request *req, *tmp;
+	int i;
 
 	/* launched pieces may still write the requests' buffers: wait them out */
 	draid_ec_ctx_synchronize(ch->ctx[gpu]);
 	draid_ec_ctx_discard_queued(ch->ctx[gpu]);
-	TAILQ_FOREACH_SAFE(req, &ch->queued, link, tmp) {
-		if (req->gpu != gpu) {
-			continue;
-		}
-		TAILQ_REMOVE(&ch->queued, req, link);
-		rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+	for (i = 0; i < n; i++) {
+		rg_complete(batch[i], SPDK_BDEV_IO_STATUS_FAILED);
 	}
 }
 
-/* One launch for everything the reactor iteration queued; requests of a flush
- * finish when its ticket does. */
+/* Finishes the requests whose launch has completed, then launches the parity
+ * work of requests that became ready -- one launch per GPU and poll.
+ *
+ * How much goes into a launch decides how well the GPU and the reactor overlap.
+ * Everything that is ready in one launch -- the obvious choice -- locks a busy
+ * channel into step: all its requests compute together, then do their base I/O
+ * together, then are resubmitted together, and the GPU idles through the
+ * reactor's part and the reactor through the GPU's.  So a launch takes at most
+ * half of the channel's requests in flight (one when there is only one), and
+ * no more than RG_MAX_INFLIGHT launches run per GPU: two groups of requests
+ * form that alternate between the GPU and the reactor, and whatever becomes
+ * ready while both launches run joins the next one. */
 static int
 rg_poll(void *arg)
 {
 	struct rg_channel *ch = arg;
 	struct rg_info *info = ch->info;
 	struct rg_request *req, *tmp;
+	struct rg_request **batch = ch->batch;
+	uint64_t running_from[RG_MAX_GPUS] = { 0 };	/* lowest ticket found still running */
 	int g, busy = 0;
 
-	for (g = 0; g < info->ngpus; g++) {
-		uint64_t ticket;
+	/* tickets of one context finish in order and `running` is in launch order, so
+	 * one query per context and poll tells "still running" for all that follow */
+	TAILQ_FOREACH_SAFE(req, &ch->running, link, tmp) {
 		int rc;
 
-		if (draid_ec_ctx_queued(ch->ctx[g]) == 0) {
+		g = req->gpu;
+		if (running_from[g] && req->ticket >= running_from[g]) {
 			continue;
 		}
-		busy = 1;
-		rc = draid_ec_ctx_flush_ticket(ch->ctx[g], &ticket);
-		if (spdk_unlikely(rc != 0)) {
-			SPDK_ERRLOG("parity flush failed (%d): %s\n", rc, draid_ec_last_error());
-			rg_fail_queued(ch, g);
-			continue;
+		if (req->ticket <= ch->done_ticket[g]) {
+			rc = 0;
+		} else {
+			RG_TIC(t_q);
+			rc = draid_ec_ctx_ticket_query(ch->ctx[g], req->ticket);
+			RG_TOC(t_q, poll);
 		}
-		RG_COUNT(info, flushes);
-		TAILQ_FOREACH_SAFE(req, &ch->queued, link, tmp) {
-			if (req->gpu != g) {
-				continue;
-			}
-			TAILQ_REMOVE(&ch->queued, req, link);
-			RG_COUNT(info, gpu_requests);
-			req->ticket = ticket;
-			TAILQ_INSERT_TAIL(&ch->running, req, link);
-		}
-	}
-	TAILQ_FOREACH_SAFE(req, &ch->running, link, tmp) {
-		const int rc = draid_ec_ctx_ticket_query(ch->ctx[req->gpu], req->ticket);
-
 		if (rc == 1) {
-			continue;	/* still running (another GPU's requests may be done) */
+			running_from[g] = req->ticket;	/* another GPU's requests may be done */
+			continue;
 		}
 		busy = 1;
 		TAILQ_REMOVE(&ch->running, req, link);
+		/* over, one way or the other: it no longer counts as in flight */
+		ch->done_ticket[g] = spdk_max(ch->done_ticket[g], req->ticket);
 		if (spdk_unlikely(rc != 0)) {
 			SPDK_ERRLOG("parity work failed (%d): %s\n", rc, draid_ec_last_error());
 			rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
 			continue;
 		}
 		rg_gpu_done(req);
+	}
+	if (TAILQ_EMPTY(&ch->ready)) {
+		return busy ? SPDK_POLLER_BUSY : SPDK_POLLER_IDLE;
+	}
+	for (g = 0; g < info->ngpus; g++) {
+		const int take = spdk_max(1, (ch->busy_reqs + 1) / 2);
+		uint64_t ticket;
+		int rc, n = 0, i;
+
+		if (ch->last_ticket[g] - ch->done_ticket[g] >= RG_MAX_INFLIGHT) {
+			busy = 1;
+			continue;	/* what is ready waits, and grows, until a launch finishes */
+		}
+		TAILQ_FOREACH_SAFE(req, &ch->ready, link, tmp) {
+			if (req->gpu != g) {
+				continue;
+			}
+			if (n == take) {
+				break;
+			}
+			TAILQ_REMOVE(&ch->ready, req, link);
+			rc = req->kind == RG_READ ? rg_queue_read_rebuild(req) : rg_queue_write(req);
+			if (spdk_unlikely(rc != 0)) {
+				/* nothing of it is queued (rg_queue_failed) */
+				rg_complete(req, SPDK_BDEV_IO_STATUS_FAILED);
+				continue;
+			}
+			batch[n++] = req;
+		}
+		if (n == 0) {
+			continue;
+		}
+		busy = 1;
+		{
+			RG_TIC(t_f);
+			rc = draid_ec_ctx_flush_ticket(ch->ctx[g], &ticket);
+			RG_TOC(t_f, flush);
+		}
+		if (spdk_unlikely(rc != 0)) {
+			SPDK_ERRLOG("parity flush failed (%d): %s\n", rc, draid_ec_last_error());
+			rg_fail_batch(ch, g, batch, n);
+			continue;
+		}
+		RG_COUNT(info, flushes);
+		ch->last_ticket[g] = ticket;
+		for (i = 0; i < n; i++) {
+			RG_COUNT(info, gpu_requests);
+			batch[i]->ticket = ticket;
+			TAILQ_INSERT_TAIL(&ch->running, batch[i], link);
+		}
 	}
 	return busy ? SPDK_POLLER_BUSY : SPDK_POLLER_IDLE;
 }
@@ -826,7 +962,7 @@ rg_io_channel_resource_deinit(void *resource)
 	struct rg_channel *ch = resource;
 	int g;
 
-	assert(TAILQ_EMPTY(&ch->queued) && TAILQ_EMPTY(&ch->running) && TAILQ_EMPTY(&ch->waiting));
+	assert(TAILQ_EMPTY(&ch->ready) && TAILQ_EMPTY(&ch->running) && TAILQ_EMPTY(&ch->waiting));
 	spdk_poller_unregister(&ch->poller);
 	for (g = 0; g < RG_MAX_GPUS; g++) {
 		if (ch->ctx[g]) {
@@ -837,13 +973,15 @@ rg_io_channel_resource_deinit(void *resource)
 	if (ch->requests) {
 		int i;
 
-		for (i = 0; i < RG_MAX_REQUESTS; i++) {
+		for (i = 0; i < ch->info->nrequests; i++) {
 			free(ch->requests[i].ios);
 			free(ch->requests[i].chunk_buf);
 		}
 		free(ch->requests);
 		ch->requests = NULL;
 	}
+	free(ch->batch);
+	ch->batch = NULL;
 	if (ch->pool) {
 		if (ch->pool_registered) {
 			/* drops the pinning and the library's cached translation of the range,
@@ -877,16 +1015,17 @@ rg_io_channel_resource_init(struct raid_bdev *raid_bdev, void *resource)
 	ch->info = info;
 	__atomic_add_fetch(&info->refs, 1, __ATOMIC_RELAXED);
 	TAILQ_INIT(&ch->free_reqs);
-	TAILQ_INIT(&ch->queued);
+	TAILQ_INIT(&ch->ready);
 	TAILQ_INIT(&ch->running);
 	TAILQ_INIT(&ch->waiting);
 
 	RAID_FOR_EACH_BASE_BDEV(raid_bdev, base_info) {
 		alignment = spdk_max(alignment, spdk_bdev_get_buf_align(base_info->bdev));
 	}
-	ch->pool = spdk_dma_malloc((size_t)RG_MAX_REQUESTS * n * strip_bytes, alignment, NULL);
-	ch->requests = calloc(RG_MAX_REQUESTS, sizeof(*ch->requests));
-	if (!ch->pool || !ch->requests) {
+	ch->pool = spdk_dma_malloc((size_t)info->nrequests * n * strip_bytes, alignment, NULL);
+	ch->requests = calloc((size_t)info->nrequests, sizeof(*ch->requests));
+	ch->batch = calloc((size_t)info->nrequests, sizeof(*ch->batch));
+	if (!ch->pool || !ch->requests || !ch->batch) {
 		goto err;
 	}
 	{
@@ -894,10 +1033,10 @@ rg_io_channel_resource_init(struct raid_bdev *raid_bdev, void *resource)
 		 * registered (or allocated through draid_ec_host_alloc) already is */
 		void *dev_ptr;
 
-		if (draid_ec_device_pointer(ch->pool, (size_t)RG_MAX_REQUESTS * n * strip_bytes,
+		if (draid_ec_device_pointer(ch->pool, (size_t)info->nrequests * n * strip_bytes,
 					    &dev_ptr) != 0) {
 			if (draid_ec_host_register(ch->pool,
-						   (size_t)RG_MAX_REQUESTS * n * strip_bytes) != 0) {
+						   (size_t)info->nrequests * n * strip_bytes) != 0) {
 				SPDK_ERRLOG("strip buffers are not GPU reachable and cannot be "
 					    "registered: %s\n", draid_ec_last_error());
 				goto err;
@@ -905,7 +1044,7 @@ rg_io_channel_resource_init(struct raid_bdev *raid_bdev, void *resource)
 			ch->pool_registered = true;
 		}
 	}
-	for (i = 0; i < RG_MAX_REQUESTS; i++) {
+	for (i = 0; i < info->nrequests; i++) {
 		struct rg_request *req = &ch->requests[i];
 
 		req->ch = ch;
@@ -956,7 +1095,7 @@ rg_start(struct raid_bdev *raid_bdev)
 	uint64_t min_blockcnt = UINT64_MAX;
 	struct raid_base_bdev_info *base_info;
 	struct rg_info *info;
-	const char *env = getenv("DRAID_RAID_GPUS");
+	const char *env = getenv("DRAID_RAID_GPUS"), *env_req = getenv("DRAID_RAID_REQUESTS");
 	int level = raid_bdev->level == RAID5 ? 5 : 6;
 	int rc, count = 0;
 
@@ -967,6 +1106,12 @@ rg_start(struct raid_bdev *raid_bdev)
 	}
 	info->raid_bdev = raid_bdev;
 	info->refs = 1;
+	/* requests a channel works on at once (raid5_simple.c:14 keeps 128); more of
+	 * them make larger launches when the queue is deep, at n strip buffers each */
+	info->nrequests = RG_REQUESTS_DEFAULT;
+	if (env_req && atoi(env_req) > 0) {
+		info->nrequests = spdk_min(spdk_max(atoi(env_req), 2), RG_REQUESTS_MAX);
+	}
 	RAID_FOR_EACH_BASE_BDEV(raid_bdev, base_info) {
 		min_blockcnt = spdk_min(min_blockcnt, base_info->bdev->blockcnt);
 	}

@@ -46,4 +46,23 @@ struct raid_gpu_stats {
 };
 void raid_gpu_get_stats(const struct raid_bdev *raid_bdev, struct raid_gpu_stats *stats);
 
+/* Where a reactor's time goes inside the module, summed over every array and
+ * channel of the process: nanoseconds and calls per section.  Only a build with
+ * -DDRAID_RAID_GPU_PROFILE measures (two clock reads around each section); any
+ * other build reports zeros. */
+struct raid_gpu_prof_section {
+	uint64_t ns, calls;
+};
+struct raid_gpu_prof {
+	struct raid_gpu_prof_section map;	/* request -> stripe, chunk ranges (draid_raid_map_request) */
+	struct raid_gpu_prof_section stripe_queue;	/* stripe cache get / enqueue / complete / put */
+	struct raid_gpu_prof_section plan;	/* preread / read planning (host layer, no context calls) */
+	struct raid_gpu_prof_section walk;	/* iovec walk + descriptors queued on the context */
+	struct raid_gpu_prof_section base_submit;	/* spdk_bdev_{read,write}v_blocks calls */
+	struct raid_gpu_prof_section flush;	/* draid_ec_ctx_flush_ticket: upload + launch */
+	struct raid_gpu_prof_section poll;	/* ticket queries of the running requests */
+	struct raid_gpu_prof_section complete;	/* raid_bdev_io_complete and what it calls */
+};
+void raid_gpu_get_prof(struct raid_gpu_prof *prof, bool reset);
+
 #endif /* DRAID_SPDK_RAID_GPU_H */

@@ -141,8 +141,9 @@ int draid_ec_encode(const draid_ec_stripe_batch *batch, void *stream);
 /* Degraded-read / rebuild reconstruct.  `fail` is a DEVICE array of
  * nstripes * 2 bytes: the (up to two) failed strip indices of each stripe
  * (0..k-1 data, k = P, k+1 = Q; DRAID_EC_FAIL_NONE = unused).  The listed
- * strips are regenerated into their table pointers.  Entries >= k+m are
- * ignored; a stripe with more failures than m is left untouched. */
+ * strips are regenerated into their table pointers.  A stripe with more
+ * failures than m, or with an entry in [k+m, 0xFF), is left untouched -- also its
+ * other, valid entry: a pair with a wild index is not trusted at all. */
 int draid_ec_reconstruct(const draid_ec_stripe_batch *batch, const uint8_t *fail,
                          void *stream);
 

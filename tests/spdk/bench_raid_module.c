@@ -12,7 +12,16 @@
  * the whole request path of one core -- mapping, the stripe queue, the parity
  * launch, base I/O and the copies -- not the kernels.
  *
- *   bench_raid_module [level n strip_kib qd seconds]     default: 6 10 64 32 2
+ * With "null" as the sixth argument the base bdevs complete every I/O without
+ * moving data (what module/bdev/null does): what is left is the module itself
+ * and, for writes and degraded reads, the GPU reading the request buffers over
+ * PCIe.  A build of the module with -DDRAID_RAID_GPU_PROFILE (the _prof binary)
+ * adds where a reactor's time goes per request: request mapping, the stripe
+ * queue, planning, the iovec walk, base I/O submission, the flush (descriptor
+ * upload + launch), ticket polling, parent completion; the rest of the reactor's
+ * time per request is the runtime stand-in and the bench's own resubmission.
+ *
+ *   bench_raid_module [level n strip_kib qd seconds [null]]   default: 6 10 64 32 2
  */
 #include "spdk/stdinc.h"
 
@@ -33,6 +42,8 @@
 			exit(1);                                                      \
 		}                                                                     \
 	} while (0)
+
+static bool g_null;
 
 struct job;
 struct task {
@@ -99,6 +110,7 @@ run_job(const char *name, struct raid_bdev *raid, struct spdk_io_channel *ch,
 {
 	struct spdk_bdev *bdev = &raid->bdev;
 	struct raid_gpu_stats s0, s1;
+	struct raid_gpu_prof pr;
 	struct job j = { .bdev = bdev, .ch = ch, .type = type, .io_blocks = io_blocks };
 	struct task *tasks = calloc((size_t)qd, sizeof(*tasks));
 	double t0, t1;
@@ -116,6 +128,7 @@ run_job(const char *name, struct raid_bdev *raid, struct spdk_io_channel *ch,
 		tasks[i].iov.iov_len = io_blocks * bdev->blocklen;
 	}
 	raid_gpu_get_stats(raid, &s0);
+	raid_gpu_get_prof(&pr, true);
 	t0 = now_s();
 	for (i = 0; i < qd; i++) {
 		task_submit(&tasks[i]);
@@ -129,10 +142,12 @@ run_job(const char *name, struct raid_bdev *raid, struct spdk_io_channel *ch,
 	}
 	t1 = now_s();
 	raid_gpu_get_stats(raid, &s1);
-	printf("{\"job\": \"%s\", \"level\": %d, \"n\": %u, \"strip_kib\": %u, \"io_kib\": %llu, \"qd\": %d, "
+	raid_gpu_get_prof(&pr, false);
+	printf("{\"job\": \"%s\", \"base_bdevs\": \"%s\", \"level\": %d, \"n\": %u, \"strip_kib\": %u, "
+	       "\"io_kib\": %llu, \"qd\": %d, "
 	       "\"seconds\": %.2f, \"ios\": %llu, \"failed\": %llu, \"iops\": %.0f, \"mib_s\": %.0f, "
-	       "\"launches\": %llu, \"requests_per_launch\": %.1f}\n",
-	       name, raid->level == RAID5 ? 5 : 6, raid->num_base_bdevs,
+	       "\"launches\": %llu, \"requests_per_launch\": %.1f",
+	       name, g_null ? "null" : "ram", raid->level == RAID5 ? 5 : 6, raid->num_base_bdevs,
 	       raid->strip_size * bdev->blocklen / 1024,
 	       (unsigned long long)(io_blocks * bdev->blocklen / 1024), qd, t1 - t0,
 	       (unsigned long long)j.done, (unsigned long long)j.failed, (double)j.done / (t1 - t0),
@@ -140,6 +155,22 @@ run_job(const char *name, struct raid_bdev *raid, struct spdk_io_channel *ch,
 	       (unsigned long long)(s1.flushes - s0.flushes),
 	       s1.flushes > s0.flushes ? (double)(s1.gpu_requests - s0.gpu_requests) /
 	       (double)(s1.flushes - s0.flushes) : 0.0);
+	printf(", \"reactor_us_per_request\": %.3f", (t1 - t0) * 1e6 / (double)j.done);
+	if (pr.map.calls) {
+		/* module sections, microseconds of reactor time per completed request */
+		const double per = 1e-3 / (double)j.done;
+		const double sum = (double)(pr.map.ns + pr.stripe_queue.ns + pr.plan.ns + pr.walk.ns +
+					    pr.base_submit.ns + pr.flush.ns + pr.poll.ns + pr.complete.ns);
+
+		printf(", \"module_us_per_request\": {\"map\": %.3f, \"stripe_queue\": %.3f, \"plan\": %.3f, "
+		       "\"walk\": %.3f, \"base_submit\": %.3f, \"flush\": %.3f, \"poll\": %.3f, "
+		       "\"complete_and_resubmit\": %.3f, \"sum\": %.3f}, \"ticket_queries_per_request\": %.1f",
+		       (double)pr.map.ns * per, (double)pr.stripe_queue.ns * per, (double)pr.plan.ns * per,
+		       (double)pr.walk.ns * per, (double)pr.base_submit.ns * per, (double)pr.flush.ns * per,
+		       (double)pr.poll.ns * per, (double)pr.complete.ns * per, sum * per,
+		       (double)pr.poll.calls / (double)j.done);
+	}
+	printf("}\n");
 	fflush(stdout);
 	CHECK(j.failed == 0);
 	for (i = 0; i < qd; i++) {
@@ -162,6 +193,7 @@ main(int argc, char **argv)
 	const uint32_t strip_kib = argc > 3 ? (uint32_t)atoi(argv[3]) : 64;
 	const int qd = argc > 4 ? atoi(argv[4]) : 32;
 	const double seconds = argc > 5 ? atof(argv[5]) : 2.0;
+	const bool null_io = argc > 6 && strcmp(argv[6], "null") == 0;
 	const uint32_t blocklen = 4096;
 	const uint32_t strip_blocks = strip_kib * 1024 / blocklen;
 	const uint64_t stripes = 256;
@@ -177,6 +209,7 @@ main(int argc, char **argv)
 		fprintf(stderr, "no GPU: %s\n", draid_ec_last_error());
 		return 2;
 	}
+	g_null = null_io;
 	CHECK(n >= 3 && n <= 32 && strip_blocks > 0 && qd > 0 && (level == 5 || level == 6));
 	k = n - (level == 5 ? 1 : 2);
 	CHECK(raid_bdev_config_add("bench", strip_kib, (uint8_t)n, level == 5 ? RAID5 : RAID6, &cfg) == 0);
@@ -184,6 +217,7 @@ main(int argc, char **argv)
 		snprintf(bname, sizeof(bname), "bench_base%d", i);
 		base[i] = stub_ram_bdev_create(bname, stripes * strip_blocks, blocklen);
 		CHECK(base[i] != NULL);
+		stub_set_null_io(base[i], null_io);
 		CHECK(raid_bdev_config_add_base_bdev(cfg, bname, (uint8_t)i) == 0);
 	}
 	CHECK(raid_bdev_create(cfg) == 0);

@@ -364,10 +364,12 @@ def test_reconstruct_ignores_unrecoverable(ec):
 
 @pytest.mark.parametrize("m", [1, 2])
 def test_single_data_strip_and_odd_failure_entries(ec, m):
-    """k = 1 (P and Q are copies of D0), and failure tables with a duplicated index,
-    an out-of-range entry beside a real one, and the real index in the second slot:
-    each stripe rebuilds exactly its one lost strip."""
-    for k, L, B in [(1, 4096 + 5, 4), (6, 2048, 5)]:
+    """k = 1 (P and Q are copies of D0), and failure tables with a duplicated index and
+    the real index in the second slot: each stripe rebuilds exactly its one lost strip.
+    A stripe with an out-of-range entry beside a real one is counted as unrecoverable and
+    left untouched, like every counted stripe: the valid index is NOT rebuilt (a table
+    with a wild entry is not to be trusted for its other one)."""
+    for k, L, B in [(1, 4096 + 5, 4), (6, 2048, 5), (9, 1024, 5)]:
         n = k + m
         rng = np.random.default_rng(k + 10 * m)
         data = np.zeros((B, n, L), np.uint8)
@@ -385,13 +387,19 @@ def test_single_data_strip_and_odd_failure_entries(ec, m):
         lost = [0, k, 0, n - 1, k - 1]
         rows = [[lost[0], lost[0]], [lost[1], 200], [0xFF, lost[2]], [n + 3, lost[3]],
                 [lost[4], 0xFF]][:B]
+        wild = [s for s in range(B) if any(e != 0xFF and e >= n for e in rows[s])]
         v = b.strips()
         for s in range(B):
             v[s, lost[s]].fill_(0xE1)
+        want = ref.copy()
+        for s in wild:
+            want[s, lost[s]] = 0xE1                      # untouched
         fail = np.array(rows, np.uint8).reshape(-1)
-        assert ec.reconstruct(b.batch(ec), dev(fail), stream) == 0
+        counter = torch.zeros(1, dtype=torch.int32, device=DEV)
+        assert ec.reconstruct_status(b.batch(ec), dev(fail), counter, stream) == 0
         sync()
-        assert (host(b.strips()) == ref).all(), (k, m)
+        assert (host(b.strips()) == want).all(), (k, m)
+        assert int(counter.item()) == len(wild) == 2
 
 
 def test_unaligned_batch(ec):
