@@ -9,11 +9,21 @@
 //   raid5_complete_reconstructed_stripe_request  raid5.c:544-594
 //   D+P / D+D recovery                            gf_vect_mul.c:242-347
 //
-// Shape: one workgroup (one 64-lane wave in production, kLanes below) owns one
-// chunk of one stripe: CB = lanes * U * 16 bytes of every strip (1 KiB).  Each
-// lane holds U 16-byte vectors per strip; with k known at compile time every
-// source load of the lane is issued before the first XOR, so a wave keeps k*U
-// KiB in flight.  HBM is the roofline: encode moves (k+m)*S algorithmic bytes per
+// Shape: a work item is one 1 KiB chunk of every strip of one stripe (64 lanes x
+// one 16-byte vector per strip).  Three workgroup shapes run items (the launch
+// policy below picks one per width, by measurement):
+//   - one 64-lane wave per item, loading all k strips (k_encode, k_reconstruct):
+//     k = 2, the RAID6 reconstruct up to k = 7, run-time widths above 20;
+//   - an item shared by 2 or 4 waves that deal the strips among themselves, each
+//     accumulating P and the Horner form of Q over its own strips, the parts
+//     combined through LDS after one barrier (k_encode_split): every encode
+//     from k = 3;
+//   - an item shared by two waves that deal the loads by strip and the
+//     arithmetic by column: raw vectors to LDS rows, one barrier, then every lane
+//     runs both syndromes down its own columns (k_reconstruct_cols): the
+//     reconstruct from k = 8.
+// With k known at compile time every strip load of a wave is issued before its
+// first XOR.  HBM is the roofline: encode moves (k+m)*S algorithmic bytes per
 // stripe and does ~2 VALU ops per byte read, far below the VALU ceiling.
 // Workgroups are independent (no inter-workgroup communication, no atomics on
 // the hot path).
@@ -51,7 +61,22 @@ int get_variant() { return g_variant; }
 // loads the reconstruct plan step costs nothing measurable at U=1 (6.296 vs a
 // no-plan diagnostic build's 6.297 TB/s).
 constexpr int enc_unroll(int) { return 1; }
-constexpr int rec_unroll(int) { return 1; }
+// The narrow RAID6 reconstructs write as many strips as they read, or nearly, and a
+// 1 KiB item of 2+2 moves only 4 KiB: with two vectors per lane (2 KiB items, half
+// as many workgroups) 2+2 x 64 KiB dual runs 418 vs 483 us per 2.68 GB and 4+2
+// 430 vs 438 (at 4 waves per SIMD); 3+2 ties at best (431 vs 431-442), so it keeps
+// one (same-box A/B of whole library builds, profiles/r03/split/narrow_raid6_u2_ab.jsonl).
+// DRAID_REC_NARROW_U overrides all three, for sweeps.
+#ifndef DRAID_REC_NARROW_U
+#define DRAID_REC_NARROW_U 0
+#endif
+constexpr int rec_unroll(int k, int m)
+{
+    return (m != 2 || k > 4)   ? 1
+           : DRAID_REC_NARROW_U ? DRAID_REC_NARROW_U
+           : (k == 2 || k == 4) ? 2
+                                : 1;
+}
 
 static inline uint32_t chunks_per_stripe(uint64_t len, int nthr, int U)
 {
@@ -133,7 +158,9 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
     return hipGetLastError();
 }
 
-template <int KT, int M, class C, class Ptrs>
+// BYSTRIP: a shared item's arithmetic is dealt by strip (k_reconstruct_split)
+// instead of by column (k_reconstruct_cols).
+template <int KT, int M, class C, bool BYSTRIP = false, class Ptrs>
 static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
                                  const uint8_t* fail, uint32_t f01, uint32_t* bad, hipStream_t st)
 {
@@ -145,8 +172,12 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
     if constexpr (C::SPLIT > 1) {
         ItemGrid ig;
         const dim3 g = split_grid(cps, nstripes, ig);
-        hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
-                           static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
+        if constexpr (BYSTRIP)
+            hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
+                               static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
+        else
+            hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
+                               static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
     } else {
         hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp,
                            k, static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
@@ -213,7 +244,7 @@ constexpr int rec_waves(int k, int m)
     return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
            : m == 1             ? rec_waves_raid5(k)
            : k <= 3             ? 7  // 3+2 dual 429 vs 453 us at the compiler's choice
-           : k == 4             ? 0
+           : k == 4             ? 4  // with two vectors per lane (rec_unroll): 430 vs 441 at 0
            : k == 5             ? 6
            : k == 6             ? 5
            : k <= 12            ? 4
@@ -257,8 +288,27 @@ constexpr int rec_waves(int k, int m)
 #ifndef DRAID_REC_SPLIT
 #define DRAID_REC_SPLIT 0
 #endif
-constexpr int enc_split(int k) { return DRAID_ENC_SPLIT >= 1 ? DRAID_ENC_SPLIT : k <= 2 ? 1 : k <= 7 ? 2 : 4; }
-constexpr int rec_split(int k) { return DRAID_REC_SPLIT >= 1 ? DRAID_REC_SPLIT : k >= 8 ? 2 : 1; }
+// Widths 21..32 (batched calls only): DRAID_ENC_SPLIT_WIDE / DRAID_REC_SPLIT_WIDE.
+#ifndef DRAID_ENC_SPLIT_WIDE
+#define DRAID_ENC_SPLIT_WIDE 4
+#endif
+#ifndef DRAID_REC_SPLIT_WIDE
+#define DRAID_REC_SPLIT_WIDE 4
+#endif
+constexpr int enc_split(int k)
+{
+    return DRAID_ENC_SPLIT >= 1 ? DRAID_ENC_SPLIT : k <= 2 ? 1 : k <= 7 ? 2 : k <= 20 ? 4 : DRAID_ENC_SPLIT_WIDE;
+}
+constexpr int rec_split(int k)
+{
+    return DRAID_REC_SPLIT >= 1 ? DRAID_REC_SPLIT : k <= 7 ? 1 : k <= 20 ? 2 : DRAID_REC_SPLIT_WIDE;
+}
+// From this width up a shared reconstruct deals its arithmetic by strip, below it
+// by column.
+#ifndef DRAID_REC_STRIP_FROM
+#define DRAID_REC_STRIP_FROM 21
+#endif
+constexpr bool rec_by_strip(int k) { return k >= DRAID_REC_STRIP_FROM && rec_split(k) > 1; }
 constexpr int enc_split_waves(int k, int m)
 {
     return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES
@@ -268,10 +318,14 @@ constexpr int enc_split_waves(int k, int m)
            : k >= 17            ? 5  // 18+2 394-396 vs 398-399 us at 6, 403 at 7
                                 : 6;
 }
+#ifndef DRAID_REC_STRIP_WAVES
+#define DRAID_REC_STRIP_WAVES 6
+#endif
 constexpr int rec_split_waves(int k, int m)
 {
     return DRAID_REC_WAVES >= 0 ? DRAID_REC_WAVES
            : rec_split(k) == 1  ? rec_waves(k, m)
+           : rec_by_strip(k)    ? DRAID_REC_STRIP_WAVES
            : (k == 8 && m == 2) ? 6
            : (k == 16 && m == 1) ? 3  // 398 vs 404 us at 4
            : k >= 15             ? 4  // (k + 2) KiB of LDS per item leave room for no more
@@ -314,6 +368,10 @@ using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global
 #define DRAID_FOR_EACH_K(X) \
     X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
     X(17) X(18) X(19) X(20)
+// Wider stripes with unrolled shared-item instances in the batched calls (table and
+// strided layouts); the scatter-gather lists run them through the run-time loop.
+#define DRAID_FOR_EACH_WIDE_K(X) \
+    X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
 
 template <int M, class Ptrs>
 static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
@@ -326,6 +384,7 @@ static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint
                          EncCfg<enc_unroll(K), enc_map(K), enc_split_waves(K, M), enc_split(K)>>(  \
             pp, k, len, nstripes, nullptr, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
+        DRAID_FOR_EACH_WIDE_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
         return go_encode<0, M, false, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(pp, k, len, nstripes,
@@ -341,10 +400,11 @@ static hipError_t dispatch_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len,
     switch (k) {
 #define DRAID_CASE(K)                                                                       \
     case K:                                                                                 \
-        return go_reconstruct<K, M, RecCfg<rec_unroll(K), rec_split_waves(K, M),            \
-                                           rec_split(K)>>(pp, k, len, nstripes, fail, f01,  \
-                                                          bad, st);
+        return go_reconstruct<K, M, RecCfg<rec_unroll(K, M), rec_split_waves(K, M),            \
+                                           rec_split(K)>, rec_by_strip(K)>(                   \
+            pp, k, len, nstripes, fail, f01, bad, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
+        DRAID_FOR_EACH_WIDE_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
         return go_reconstruct<0, M, RecCfg<1, DRAID_RT_REC_WAVES>>(pp, k, len, nstripes, fail,
@@ -435,7 +495,7 @@ static hipError_t variant_reconstruct(int v, const TablePtrs& pp, uint64_t len, 
         DRAID_VARIANTS(DRAID_V)
 #undef DRAID_V
     default:
-        return go_reconstruct<K, M, RecCfg<rec_unroll(K)>>(pp, K, len, ns, fail, 0xffffu, nullptr, st);
+        return go_reconstruct<K, M, RecCfg<rec_unroll(K, M)>>(pp, K, len, ns, fail, 0xffffu, nullptr, st);
     }
 }
 
@@ -585,7 +645,7 @@ uint32_t work_chunk_bytes(int op, uint32_t k)
     switch (k) {
 #define DRAID_CASE(K)                                       \
     case K:                                                 \
-        u = op == 0 ? enc_unroll(K) : rec_unroll(K); \
+        u = op == 0 ? enc_unroll(K) : 1;             \
         break;
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
@@ -636,10 +696,10 @@ hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const*
     switch (k) {
 #define DRAID_CASE(K)                                                                         \
     case K:                                                                                   \
-        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<rec_unroll(K), DRAID_REC_WORK_WAVES(K, 1), \
+        return m == 1 ? go_reconstruct_work<K, 1, RecCfg<1, DRAID_REC_WORK_WAVES(K, 1),             \
                                                          DRAID_REC_WORK_SPLIT(K)>>(             \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st) \
-                      : go_reconstruct_work<K, 2, RecCfg<rec_unroll(K), DRAID_REC_WORK_WAVES(K, 2), \
+                      : go_reconstruct_work<K, 2, RecCfg<1, DRAID_REC_WORK_WAVES(K, 2),             \
                                                          DRAID_REC_WORK_SPLIT(K)>>(             \
                             table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)

@@ -29,7 +29,7 @@ struct RecPlan {
     bool needq;        // the Q syndrome over the survivors is needed
     bool skip;         // unrecoverable / nothing to do
     bool bad;          // more failures than M parities, or an index outside the stripe
-    uint32_t lost;     // bit j set: strip j is lost (decode_failures_mask only)
+    uint64_t lost;     // bit j set: strip j is lost (decode_failures_mask only)
     MulTable t1, t2;   // constant multipliers (see plan_constants)
 };
 
@@ -85,27 +85,43 @@ __device__ __forceinline__ RecPlan decode_failures(int k, uint32_t f0, uint32_t 
     return pl;
 }
 
-// The same decode for a stripe of at most 32 strips known at compile time, over a
-// bit mask of the lost strips: a third of the scalar instructions, and "is strip
-// j lost" becomes a one-instruction bit test per load.  Every wave of a split
-// item runs this ahead of its strip loads, so its length is item latency.
+// The same decode for a stripe of at most 64 strips known at compile time, over a
+// bit mask of the lost strips (one word up to 32 strips, two beyond): a third of
+// the scalar instructions, and "is strip j lost" becomes a one-instruction bit
+// test per load.  Every wave of a split item runs this ahead of its strip loads,
+// so its length is item latency.
 template <int K, int M>
 __device__ __forceinline__ RecPlan decode_failures_mask(uint32_t f0, uint32_t f1)
 {
-    static_assert(K + M <= 32, "one mask word");
-    constexpr uint32_t N = K + M, DATA = (K >= 32) ? 0xffffffffu : ((1u << K) - 1u);
+    static_assert(K + M <= 64, "two mask words");
+    constexpr uint32_t N = K + M;
     RecPlan pl;
     const uint32_t a = __builtin_amdgcn_readfirstlane(f0), b = __builtin_amdgcn_readfirstlane(f1);
-    const uint32_t L = (a < N ? 1u << a : 0u) | (b < N ? 1u << b : 0u);
     const bool oob = (a >= N && a != 0xffu) || (b >= N && b != 0xffu);
-    const uint32_t D = L & DATA;
-    pl.lost = L;
-    pl.nd = __builtin_popcount(D);
-    pl.x = __builtin_ffs(static_cast<int>(D)) - 1;                  // lowest lost data strip, or -1
-    pl.y = pl.nd == 2 ? 31 - __builtin_clz(D) : -1;
-    pl.lostP = (L >> K) & 1u;
-    pl.lostQ = M == 2 && ((L >> (K + 1)) & 1u);
-    const int nf = __builtin_popcount(L);
+    int nf;
+    if constexpr (N <= 32) {
+        constexpr uint32_t DATA = (K >= 32) ? 0xffffffffu : ((1u << K) - 1u);
+        const uint32_t L = (a < N ? 1u << a : 0u) | (b < N ? 1u << b : 0u);
+        const uint32_t D = L & DATA;
+        pl.lost = L;
+        pl.nd = __builtin_popcount(D);
+        pl.x = __builtin_ffs(static_cast<int>(D)) - 1;              // lowest lost data strip, or -1
+        pl.y = pl.nd == 2 ? 31 - __builtin_clz(D) : -1;
+        pl.lostP = (L >> K) & 1u;
+        pl.lostQ = M == 2 && ((L >> (K + 1)) & 1u);
+        nf = __builtin_popcount(L);
+    } else {
+        constexpr uint64_t DATA = (1ull << K) - 1ull;
+        const uint64_t L = (a < N ? 1ull << a : 0ull) | (b < N ? 1ull << b : 0ull);
+        const uint64_t D = L & DATA;
+        pl.lost = L;
+        pl.nd = __builtin_popcountll(D);
+        pl.x = __builtin_ffsll(static_cast<long long>(D)) - 1;
+        pl.y = pl.nd == 2 ? 63 - __builtin_clzll(D) : -1;
+        pl.lostP = (L >> K) & 1u;
+        pl.lostQ = M == 2 && ((L >> (K + 1)) & 1u);
+        nf = __builtin_popcountll(L);
+    }
     pl.skip = (nf == 0) || (nf > M) || oob;  // a counted stripe is left untouched
     pl.bad = oob || nf > M;
     pl.needq = (M == 2) && (pl.nd == 2 || (pl.nd == 1 && pl.lostP) || pl.lostQ);
@@ -479,6 +495,52 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct(P
     }
 }
 
+// The rebuilt strips' ND dwords per lane from the two syndromes of their columns
+// (pt: P ^ survivors, qt: Q ^ Horner sum of the survivors): the output stage both
+// shared reconstructs end in.
+template <int M, int POL, int ND>
+__device__ __forceinline__ void store_rebuilt(const RecPlan& pl, const uint8_t* pP,
+                                              const uint8_t* pQ, const uint8_t* pX,
+                                              const uint8_t* pY, uint32_t ob,
+                                              const uint32_t (&pt)[ND], const uint32_t (&qt)[ND])
+{
+    uint32_t o1[ND], o2[ND];
+    if constexpr (M == 1) {
+        st_words<POL, ND>(pl.nd == 0 ? pP : pX, ob, pt);  // RAID5: XOR of the survivors
+    } else if (pl.nd == 0) {
+        if (pl.lostP)
+            st_words<POL, ND>(pP, ob, pt);
+        if (M == 2 && pl.lostQ)
+            st_words<POL, ND>(pQ, ob, qt);
+    } else if (pl.nd == 1) {
+        if (!pl.lostP) {
+            st_words<POL, ND>(pX, ob, pt);
+            if (M == 2 && pl.lostQ) {
+#pragma unroll
+                for (int n = 0; n < ND; ++n)
+                    o2[n] = qt[n] ^ gf_mulc(pl.t1, pt[n]);
+                st_words<POL, ND>(pQ, ob, o2);
+            }
+        } else {
+#pragma unroll
+            for (int n = 0; n < ND; ++n) {
+                o1[n] = gf_mulc(pl.t1, qt[n]);
+                o2[n] = pt[n] ^ o1[n];
+            }
+            st_words<POL, ND>(pX, ob, o1);
+            st_words<POL, ND>(pP, ob, o2);
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+            o1[n] = gf_mulc(pl.t1, pt[n]) ^ gf_mulc(pl.t2, qt[n]);
+            o2[n] = pt[n] ^ o1[n];
+        }
+        st_words<POL, ND>(pX, ob, o1);
+        st_words<POL, ND>(pY, ob, o2);
+    }
+}
+
 // ---- shared reconstruct: loads dealt by strip, arithmetic dealt by column
 //
 // Dealing the reconstruct's ARITHMETIC by strip as the encode does (a Horner chain
@@ -516,7 +578,9 @@ __device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, Rec
     const uint8_t* pQ = (M == 2) ? pp.get(s, KT + 1) : pP;
     const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
     const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
-    const uint32_t lost = pl.lost;
+    // (one word where the stripe fits one: the bit tests stay 32-bit scalar ops)
+    const std::conditional_t<(KT + M <= 32), uint32_t, uint64_t> lost =
+        static_cast<std::conditional_t<(KT + M <= 32), uint32_t, uint64_t>>(pl.lost);
     const bool haveP = !pl.lostP, haveQ = M == 2 && QS && pl.needq && !pl.lostQ;
     // phase 1: this wave's strips -> LDS rows (zeros for the ones it skips)
     wave_case<0, SPLIT>(w, [=, &pp, &lds](auto wc) __attribute__((always_inline)) {
@@ -580,41 +644,7 @@ __device__ __forceinline__ void recover_cols_vec(const Ptrs& pp, uint32_t s, Rec
     }
     if (!okw)
         return;
-    uint32_t o1[ND], o2[ND];
-    if constexpr (M == 1) {
-        st_words<POL, ND>(pl.nd == 0 ? pP : pX, ob, pt);  // RAID5: XOR of the survivors
-    } else if (pl.nd == 0) {
-        if (pl.lostP)
-            st_words<POL, ND>(pP, ob, pt);
-        if (M == 2 && pl.lostQ)
-            st_words<POL, ND>(pQ, ob, qt);
-    } else if (pl.nd == 1) {
-        if (!pl.lostP) {
-            st_words<POL, ND>(pX, ob, pt);
-            if (M == 2 && pl.lostQ) {
-#pragma unroll
-                for (int n = 0; n < ND; ++n)
-                    o2[n] = qt[n] ^ gf_mulc(pl.t1, pt[n]);
-                st_words<POL, ND>(pQ, ob, o2);
-            }
-        } else {
-#pragma unroll
-            for (int n = 0; n < ND; ++n) {
-                o1[n] = gf_mulc(pl.t1, qt[n]);
-                o2[n] = pt[n] ^ o1[n];
-            }
-            st_words<POL, ND>(pX, ob, o1);
-            st_words<POL, ND>(pP, ob, o2);
-        }
-    } else {
-#pragma unroll
-        for (int n = 0; n < ND; ++n) {
-            o1[n] = gf_mulc(pl.t1, pt[n]) ^ gf_mulc(pl.t2, qt[n]);
-            o2[n] = pt[n] ^ o1[n];
-        }
-        st_words<POL, ND>(pX, ob, o1);
-        st_words<POL, ND>(pY, ob, o2);
-    }
+    store_rebuilt<M, POL, ND>(pl, pP, pQ, pX, pY, ob, pt, qt);
 }
 
 // Chunk c of stripe (or segment) s with its failure pair decoded: the 16-byte vectors
@@ -677,6 +707,155 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_c
     const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
     if (!pl.skip)
         reconstruct_item_cols<KT, M, C>(pp, s, c, len, cps, pl, aligned, lds);
+    if (count_bad)
+        atomicAdd(bad, 1u);
+}
+
+// ---- shared reconstruct of wide stripes: loads AND arithmetic dealt by strip
+//
+// The column division parks every strip of the item in LDS, (k + 2) KiB per item:
+// from k = 21 up that is what limits how many items a CU holds (32+2: four), and
+// each wave still loads k / 2 or k / 4 strips for the same single barrier.  Wide
+// stripes therefore divide the arithmetic by strip too, as the encode does: wave w
+// accumulates P and the Horner form of Q over the survivors among its strips
+// (a lost strip arrives as zeros), scales its Q part by the constant 2^(first
+// strip of the wave) -- 9 VALU per dword once per wave, which at six to eight
+// strips per wave costs little, where at two to four it was what sank this
+// division below k = 16 -- and the surviving P and Q ride on the last and the
+// first wave (whose scale is 1).  The parts meet in 2 * SPLIT KiB of LDS, and after
+// the barrier every wave finishes 16 / SPLIT bytes per lane of the rebuilt strips
+// from the XOR of the parts: the syndromes themselves.
+template <int KT, int M, int SPLIT, int POL, bool BOUNDED, bool QS, class Ptrs>
+__device__ __forceinline__ void recover_split_vec(const Ptrs& pp, uint32_t s, RecPlan& pl,
+                                                  uint32_t w, uint32_t lane, uint32_t i,
+                                                  uint32_t nvec, SplitLds<SPLIT>& lds)
+{
+    using MW = Mem<u32x4>;
+    static_assert(SPLIT == 2 || SPLIT == 4, "every wave finishes 16 / SPLIT bytes per lane");
+    constexpr int KW = (KT + SPLIT - 1) / SPLIT;
+    const bool ok = !BOUNDED || i < nvec;
+    const uint8_t* pP = pp.get(s, KT);
+    const uint8_t* pQ = (M == 2) ? pp.get(s, KT + 1) : pP;
+    const uint8_t* pX = pl.x >= 0 ? pp.get(s, pl.x) : nullptr;
+    const uint8_t* pY = pl.y >= 0 ? pp.get(s, pl.y) : nullptr;
+    const std::conditional_t<(KT + M <= 32), uint32_t, uint64_t> lost =
+        static_cast<std::conditional_t<(KT + M <= 32), uint32_t, uint64_t>>(pl.lost);
+    const bool haveP = !pl.lostP, haveQ = M == 2 && QS && pl.needq && !pl.lostQ;
+    const PartPQ part = wave_case<0, SPLIT>(w, [=, &pp](auto wc) __attribute__((always_inline)) {
+        constexpr int W = decltype(wc)::value;
+        constexpr int J0 = W * KW;
+        u32x4 d[KW], pv = 0, qv = 0;
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j) {
+            d[j] = 0;
+            if (J0 + j < KT)
+                d[j] = ok ? MW::template ld_if<POL>(pp.get(s, J0 + j), i, !((lost >> (J0 + j)) & 1u))
+                          : u32x4(0);
+        }
+        if constexpr (W == SPLIT - 1)
+            pv = ok ? MW::template ld_if<POL>(pP, i, haveP) : u32x4(0);
+        if constexpr (W == 0)
+            qv = ok ? MW::template ld_if<POL>(pQ, i, haveQ) : u32x4(0);
+        u32x4 p = 0, q = 0;
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j) {
+            if (J0 + j < KT) {
+                p ^= d[j];
+                if constexpr (M == 2 && QS)
+                    q = gf_mul2(q) ^ d[j];
+            }
+        }
+        if constexpr (M == 2 && QS && J0 != 0)
+            q = gf_mulc(make_mul_table(gf_exp2_const(J0)), q);
+        return PartPQ{p ^ pv, q ^ qv};
+    });
+    lds.p[w][lane] = part.p;
+    if constexpr (M == 2 && QS)
+        lds.q[w][lane] = part.q;
+    if constexpr (M == 2) {
+        const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
+        pl.t1 = mul.t1;
+        pl.t2 = mul.t2;
+    }
+    __syncthreads();
+    constexpr int ND = 4 / SPLIT;
+    const uint32_t t = (w * 64u + lane) * ND;
+    const uint32_t ob = ((i - lane) << 4) + t * 4u;
+    const bool okw = !BOUNDED || ob < (nvec << 4);
+    const uint32_t* LP = reinterpret_cast<const uint32_t*>(lds.p);
+    const uint32_t* LQ = reinterpret_cast<const uint32_t*>(lds.q);
+    uint32_t pt[ND], qt[ND];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+        pt[n] = 0;
+        qt[n] = 0;
+#pragma unroll
+        for (int r = 0; r < SPLIT; ++r) {
+            pt[n] ^= LP[r * 256 + t + n];
+            if constexpr (M == 2 && QS)
+                qt[n] ^= LQ[r * 256 + t + n];
+        }
+    }
+    if (!okw)
+        return;
+    store_rebuilt<M, POL, ND>(pl, pP, pQ, pX, pY, ob, pt, qt);
+}
+
+template <int KT, int M, class C, class Ptrs>
+__device__ __forceinline__ void reconstruct_item_split(const Ptrs& pp, uint32_t s, uint32_t c,
+                                                       uint32_t len, uint32_t cps, RecPlan& pl,
+                                                       bool aligned, SplitLds<C::SPLIT>& lds)
+{
+    constexpr int SPLIT = C::SPLIT, POL = C::POL;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t nvec = len >> 4;
+    auto none = [](RecPlan&) {};
+    if (aligned) {
+        const uint32_t i = c * 64u + lane;
+        if ((c + 1) * 64u <= nvec) {
+            if (M == 2 && !pl.needq)
+                recover_split_vec<KT, M, SPLIT, POL, false, false>(pp, s, pl, w, lane, i, nvec, lds);
+            else
+                recover_split_vec<KT, M, SPLIT, POL, false, true>(pp, s, pl, w, lane, i, nvec, lds);
+        } else {
+            recover_split_vec<KT, M, SPLIT, POL, true, true>(pp, s, pl, w, lane, i, nvec, lds);
+        }
+        const uint32_t tail = len & 15u;
+        if (w == 0 && tail && c == cps - 1 && lane < tail)
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl,
+                                                                   nvec * 16 + lane, 64, len, none);
+    } else if (w == 0) {
+        const PlanMul mul = plan_constants_scalar(pl.nd, pl.x, pl.y, pl.lostP, pl.lostQ);
+        pl.t1 = mul.t1;
+        pl.t2 = mul.t2;
+        const uint32_t b1 = min(len, (c + 1) * 1024u);
+        for (uint32_t b = c * 1024u + lane; b < b1; b += 64)
+            recover_elems<0, M, 1, 0, true, false, true, uint32_t>(pp, s, KT, pl, b, 64, b1, none);
+    }
+}
+
+template <int KT, int M, class C, class Ptrs>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_split(
+    Ptrs pp, uint32_t len, uint32_t cps, uint32_t nstripes, const uint8_t* fail, uint32_t f01,
+    uint32_t* bad, ItemGrid ig)
+{
+    static_assert(KT > 0 && C::SPLIT > 1 && C::MAP == 0, "one shared item per workgroup, stripe order");
+    __shared__ SplitLds<C::SPLIT> lds;
+    uint32_t c, s;
+    ig.coords(c, s);
+    if (s >= nstripes)
+        return;
+    const bool aligned = stripe_aligned<KT, M>(pp, s, KT);
+    uint32_t f0 = f01 & 0xffu, f1 = (f01 >> 8) & 0xffu;
+    if (fail) {
+        const uint32_t f = load_fail_pair(fail, s);
+        f0 = f & 0xffu;
+        f1 = f >> 8;
+    }
+    RecPlan pl = decode_failures_mask<KT, M>(f0, f1);
+    const bool count_bad = bad && pl.bad && c == 0 && threadIdx.x == 0;
+    if (!pl.skip)
+        reconstruct_item_split<KT, M, C>(pp, s, c, len, cps, pl, aligned, lds);
     if (count_bad)
         atomicAdd(bad, 1u);
 }

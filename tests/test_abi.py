@@ -106,3 +106,24 @@ def test_argument_errors_before_any_launch():
     assert L.draid_ec_device_alloc(None, C.c_size_t(64)) == 1
     assert L.draid_ec_host_device_pointer(dummy, None) == 1
     assert L.draid_ec_ctx_set_autoflush(None, C.c_uint64(1024)) == 1
+
+
+def test_every_registered_kernel_has_device_code():
+    """The host half of the library registers its kernels by mangled name and the GPU half
+    must hold a kernel descriptor (`<name>.kd`) for each: hipcc compiles the two halves in
+    separate passes over the source, and a library whose halves disagree (a source edited
+    while it was being compiled) aborts the process at the first launch."""
+    import subprocess
+    import draid_ec
+    out = subprocess.run(["strings", "-a", draid_ec.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout.splitlines()
+    device = {s[:-3] for s in out if s.endswith(".kd")}
+    # what the host registers: the kernels' mangled names as plain strings (the stubs
+    # and the descriptors' own attributes carry other spellings)
+    registered = {s for s in out if s.startswith("_ZN5draid") and "__device_stub__" not in s
+                  and "." not in s and s.split("I")[0].split("E")[0][len("_ZN5draid"):].lstrip(
+                      "0123456789").startswith("k_")}
+    assert len(device) > 200 and len(registered) > 200
+    missing = registered - device
+    assert not missing, sorted(missing)[:3]
+    assert device <= registered | device and len(registered & device) == len(registered)

@@ -195,7 +195,8 @@ def test_gf_vect_mul_any_table_any_length(ec, L):
 
 
 @pytest.mark.parametrize("k,m", [(2, 1), (4, 1), (8, 1), (16, 1), (8, 2), (9, 2), (10, 2), (12, 2), (14, 2),
-                                 (16, 2), (18, 2), (20, 1), (40, 2)])
+                                 (16, 2), (18, 2), (20, 1), (40, 2), (24, 2), (31, 2), (32, 2),
+                                 (32, 1), (29, 1)])
 def test_recover_every_failure_set(ec, k, m):
     L = 4096
     rng = np.random.default_rng(k)
@@ -286,9 +287,13 @@ CONFIGS = [  # (k, m, strip bytes, stripes) -- BASELINE.json configs at reduced 
     (16, 2, 262144, 16),
     (14, 2, 4096, 33),
     (11, 2, 4096 + 48, 7),   # odd width, ragged length
-    (21, 2, 4096 + 48, 7),   # run-time width: two full blocks of 8 strips and a ragged top block
-    (24, 1, 2048, 9),        # run-time width, whole blocks only
+    (21, 2, 4096 + 48, 7),   # an odd wide width (shared items, ragged last wave)
+    (24, 1, 2048, 9),
+    (37, 2, 4096 + 48, 7),   # run-time width: four full blocks of 8 strips and a ragged top block
+    (40, 1, 2048, 9),        # run-time width, whole blocks only
     (33, 2, 1024 + 7, 5),    # run-time width, five blocks, byte tail
+    (32, 2, 2048 + 16, 6),   # the widest unrolled width (two-word failure mask)
+    (27, 1, 1024 + 5, 4),
     (6, 1, 1000, 5),         # ragged length, odd size
 ]
 
@@ -538,7 +543,11 @@ def test_full_size_linearity(ec, k, m, L, B):
 
 # ------------------------------------------------------------ items shared by several waves
 
-SPLIT_K = [5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20]   # stripe widths whose items are dealt over 2 or 4 waves
+# every unrolled width: 2..4 (one wave per item; the RAID6 reconstructs of 2 and 4 with
+# two vectors per lane), 5..32 with items dealt over 2 or 4 waves (21..32 have unrolled
+# instances in the batched calls only; 31 and 32 with P and Q take a two-word failure
+# mask)
+SPLIT_K = list(range(2, 33))
 
 
 @pytest.mark.parametrize("m", [1, 2])
@@ -549,7 +558,8 @@ def test_shared_items_every_length_class(ec, k, m):
     rebuilt, with the failure table at each alignment of its first byte (the kernel
     reads it through aligned words)."""
     stream = torch.cuda.current_stream().cuda_stream
-    for L, B in [(3 * 1024, 9), (2 * 1024 + 16 * 5, 7), (1024 + 16 * 3 + 7, 6), (48, 5), (5, 4)]:
+    for L, B in [(3 * 1024, 9), (2 * 1024 + 16 * 5, 7), (1024 + 16 * 3 + 7, 6), (48, 5), (5, 4),
+                 (5 * 1024, 3), (4 * 1024 + 16, 3)]:
         rng = np.random.default_rng(k * 131 + m * 7 + L)
         b = Batch(k, m, L, B, gap=16 + (-L) % 16, seed=k + L)   # every strip 16-byte aligned
         assert b.table[0].item() % 16 == 0 and b.strip_stride % 16 == 0

@@ -21,7 +21,8 @@ rng = np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 20261113)
 stream = torch.cuda.current_stream().cuda_stream
 lens = [1, 7, 16, 48, 1000, 1024, 1040, 2048 + 16, 4096, 4096 + 5, 12 * 1024, 65536, 65536 + 3]
 for c in range(cases):
-    k = int(rng.integers(2, 21)) if rng.random() < 0.8 else int(rng.integers(21, 70))
+    # four in five up to 32 (every unrolled width), the rest run-time widths up to 69
+    k = int(rng.integers(2, 33)) if rng.random() < 0.8 else int(rng.integers(33, 70))
     m = int(rng.integers(1, 3))
     L = int(rng.choice(lens)) if rng.random() < 0.7 else int(rng.integers(1, 20000))
     B = int(rng.integers(1, 40))

@@ -6,7 +6,9 @@
 // 64-lane wave loads 1 KiB of every strip.  SPLIT = 2 / 4: a workgroup of SPLIT
 // waves, each loading k/SPLIT strips, partial P and Q (the latter scaled by
 // 2^(first strip of the wave)) combined through LDS; wave 0 stores P, the last
-// wave stores Q.  Prints microseconds per launch and algorithmic GB/s, and checks
+// wave stores Q.  U = 2: an item is 2 KiB of every strip (two 16-byte vectors per
+// lane and strip), so a workgroup's barrier and LDS exchange serve twice the
+// bytes and half as many workgroups are dispatched.  Prints microseconds per launch and algorithmic GB/s, and checks
 // every variant's parity against SPLIT = 1.
 //
 //   wide_probe K STRIP_KIB STRIPES [launches]
@@ -51,14 +53,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* p, uint32_
                                              0x00020000);
 }
 
-template <int K, int SPLIT, int WAVES>
+template <int K, int SPLIT, int WAVES, int U>
 __global__ __launch_bounds__(64 * SPLIT)
     __attribute__((amdgpu_waves_per_eu(WAVES ? WAVES : 1, WAVES ? WAVES : 8))) void k_enc(
         uint8_t* base, uint32_t strip, uint64_t pitch, uint32_t cps, uint32_t nstripes, int xcd)
 {
     constexpr int KW = (K + SPLIT - 1) / SPLIT;  // a ragged last wave reads zeros past strip K-1
-    __shared__ u32x4 sp[SPLIT > 1 ? SPLIT : 1][64];
-    __shared__ u32x4 sq[SPLIT > 1 ? SPLIT : 1][64];
+    __shared__ u32x4 sp[SPLIT > 1 ? SPLIT : 1][U][64];
+    __shared__ u32x4 sq[SPLIT > 1 ? SPLIT : 1][U][64];
     uint32_t b = blockIdx.x;
     if (xcd) {
         const uint32_t total = cps * nstripes, q = total >> 3, r = total & 7u;
@@ -68,40 +70,61 @@ __global__ __launch_bounds__(64 * SPLIT)
     const uint32_t s = b / cps, c = b - s * cps;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const uint8_t* st = base + static_cast<uint64_t>(s) * pitch;
-    const int off = static_cast<int>((c * 64u + lane) << 4);
-    u32x4 p = 0, q = 0;
+    // cps counts 1 KiB chunks; an item is U of them, 1 KiB apart
+    int off[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        off[u] = static_cast<int>(((c * U + u) * 64u + lane) << 4);
+    u32x4 p[U], q[U], d[KW][U];
 #pragma unroll
     for (int j = KW - 1; j >= 0; --j) {
         const uint32_t jj = w * KW + j;
         const uint8_t* src = st + static_cast<uint64_t>(jj < K ? jj : 0) * strip;
-        const u32x4 d =
-            __builtin_amdgcn_raw_buffer_load_b128(rsrc(src, jj < K ? strip : 0u), off, 0, 2);
-        p ^= d;
-        q = mul2(q) ^ d;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            d[j][u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(src, jj < K ? strip : 0u), off[u],
+                                                            0, 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        p[u] = 0;
+        q[u] = 0;
+#pragma unroll
+        for (int j = KW - 1; j >= 0; --j) {
+            p[u] ^= d[j][u];
+            q[u] = mul2(q[u]) ^ d[j][u];
+        }
     }
     uint8_t* dp = const_cast<uint8_t*>(st) + static_cast<uint64_t>(K) * strip;
     uint8_t* dq = dp + strip;
     if constexpr (SPLIT == 1) {
-        __builtin_amdgcn_raw_buffer_store_b128(p, rsrc(dp), off, 0, 18);
-        __builtin_amdgcn_raw_buffer_store_b128(q, rsrc(dq), off, 0, 18);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            __builtin_amdgcn_raw_buffer_store_b128(p[u], rsrc(dp), off[u], 0, 18);
+            __builtin_amdgcn_raw_buffer_store_b128(q[u], rsrc(dq), off[u], 0, 18);
+        }
     } else {
-        for (uint32_t i = 0; i < w * KW; ++i)
-            q = mul2(q);
-        sp[w][lane] = p;
-        sq[w][lane] = q;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            for (uint32_t i = 0; i < w * KW; ++i)
+                q[u] = mul2(q[u]);
+            sp[w][u][lane] = p[u];
+            sq[w][u][lane] = q[u];
+        }
         __syncthreads();
-        if (w == 0) {
-            u32x4 a = sp[0][lane];
+        // the U * 2 output vectors of the item are finished by as many waves as
+        // there are: wave t takes output t, t + SPLIT, ...
+#pragma unroll
+        for (int o = 0; o < 2 * U; ++o) {
+            if (static_cast<uint32_t>(o % SPLIT) != w)
+                continue;
+            const int u = o >> 1;
+            const bool isq = o & 1;
+            u32x4 a = isq ? sq[0][u][lane] : sp[0][u][lane];
 #pragma unroll
             for (int t = 1; t < SPLIT; ++t)
-                a ^= sp[t][lane];
-            __builtin_amdgcn_raw_buffer_store_b128(a, rsrc(dp), off, 0, 18);
-        } else if (w == SPLIT - 1) {
-            u32x4 a = sq[0][lane];
-#pragma unroll
-            for (int t = 1; t < SPLIT; ++t)
-                a ^= sq[t][lane];
-            __builtin_amdgcn_raw_buffer_store_b128(a, rsrc(dq), off, 0, 18);
+                a ^= isq ? sq[t][u][lane] : sp[t][u][lane];
+            __builtin_amdgcn_raw_buffer_store_b128(a, rsrc(isq ? dq : dp), off[u], 0, 18);
         }
     }
 }
@@ -118,7 +141,7 @@ __global__ void k_fill(uint32_t* p, uint64_t n)
 struct Run {
     const char* name;
     void (*fn)(uint8_t*, uint32_t, uint64_t, uint32_t, uint32_t, int);
-    int split;
+    int split, u;
 };
 
 template <int K>
@@ -131,9 +154,12 @@ static void study(uint32_t strip, uint32_t nstripes, int launches)
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(buf), bytes / 4);
     CK(hipDeviceSynchronize());
     const uint32_t cps = strip / 1024;
-#define V(S, W) { "split" #S " w" #W, k_enc<K, S, W>, S }
-#define VS(S) V(S, 0), V(S, 4), V(S, 5), V(S, 6), V(S, 7), V(S, 8)
-    const Run runs[] = { V(1, 0), V(1, 4), V(1, 6), VS(2), VS(3), VS(4), VS(6), VS(8) };
+#define V(S, W, U) { "split" #S " w" #W " u" #U, k_enc<K, S, W, U>, S, U }
+#define VS(S) V(S, 0, 1), V(S, 5, 1), V(S, 6, 1), V(S, 7, 1), V(S, 8, 1)
+#define VU(S) V(S, 0, 2), V(S, 3, 2), V(S, 4, 2), V(S, 5, 2), V(S, 6, 2), V(S, 8, 2)
+    const Run runs[] = { V(1, 0, 1), V(1, 4, 1), V(1, 6, 1), VS(2), VS(4), VS(8), V(1, 0, 2), V(1, 3, 2),
+                         VU(2), VU(4), VU(8) };
+#undef VU
 #undef VS
 #undef V
     std::vector<uint8_t> want(2 * static_cast<size_t>(strip)), got(2 * static_cast<size_t>(strip));
@@ -143,15 +169,16 @@ static void study(uint32_t strip, uint32_t nstripes, int launches)
     const double algo = static_cast<double>(bytes);
     for (int xcd = 0; xcd < 1; ++xcd) {
         for (const Run& r : runs) {
-            const dim3 grid(cps * nstripes), block(64 * r.split);
+            const dim3 grid(cps / r.u * nstripes), block(64 * r.split);
+            const uint32_t cps_items = cps / r.u;
             // parity of the last stripe: clear, compute, compare with split1
             CK(hipMemset(buf + pitch * (nstripes - 1) + static_cast<uint64_t>(K) * strip, 0, 2ull * strip));
             for (int i = 0; i < 5; ++i)
-                hipLaunchKernelGGL(r.fn, grid, block, 0, 0, buf, strip, pitch, cps, nstripes, xcd);
+                hipLaunchKernelGGL(r.fn, grid, block, 0, 0, buf, strip, pitch, cps_items, nstripes, xcd);
             CK(hipGetLastError());
             CK(hipEventRecord(e0, 0));
             for (int i = 0; i < launches; ++i)
-                hipLaunchKernelGGL(r.fn, grid, block, 0, 0, buf, strip, pitch, cps, nstripes, xcd);
+                hipLaunchKernelGGL(r.fn, grid, block, 0, 0, buf, strip, pitch, cps_items, nstripes, xcd);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float ms = 0;
