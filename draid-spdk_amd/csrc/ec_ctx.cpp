@@ -75,9 +75,19 @@ private:
     size_t n_ = 0, cap_ = 0;
 };
 
+// Slots (8 bytes each) of one segment's row.  A row of pointers: k + m of them,
+// plus one for a reconstruct's failure pair.  A compact row: the base pointer, then
+// the int32 offset of every strip from it, then (reconstruct) the failure pair in
+// an int32 slot of its own -- 48 instead of 80 bytes for an 8+2 encode segment.
+constexpr uint32_t row_slots(int op, uint32_t n, bool compact)
+{
+    return compact ? (8u + 4u * n + (op == 1 ? 4u : 0u) + 7u) / 8u : n + (op == 1 ? 1u : 0u);
+}
+
 struct Group {
-    Group(int op_, uint32_t k_, uint32_t m_, uint32_t level_)
-        : op(op_), level(level_), k(k_), m(m_), w(k_ + m_ + (op_ == 1))
+    Group(int op_, uint32_t k_, uint32_t m_, uint32_t level_, bool compact_)
+        : op(op_), level(level_), k(k_), m(m_), compact(compact_),
+          w(row_slots(op_, k_ + m_, compact_))
     {
     }
     Group(const Group&) = delete;
@@ -92,9 +102,10 @@ struct Group {
     uint32_t level;  // fences in front of its segments within their requests (draid_ec_ctx_fence)
     uint64_t first_seq = 0;         // queue position of the batch's first segment in this group
     uint32_t k, m;                  // op 2: k = 2 * touched chunks (old/new list pairs)
-    uint32_t w;                     // pointer slots per segment: k+m, +1 for op 1
-    PinnedPtrs ptrs;                // [nseg][w]; op 1: slot k+m holds the failure pair
-                                    // in its first two bytes (uploaded with the pointers)
+    bool compact;                   // rows of base + int32 offsets instead of pointers
+    uint32_t w;                     // 8-byte slots per segment (row_slots)
+    PinnedPtrs ptrs;                // [nseg][w]; op 1: the slot behind the strips holds the
+                                    // failure pair in its first two bytes (uploaded with the row)
     std::vector<uint32_t> len;      // [nseg]
     std::vector<uint8_t> fail;      // op 2: [nseg][k/2] exponents
     // Double-buffered pointer storage: a flush whose pieces DMA straight from
@@ -146,6 +157,7 @@ struct draid_ec_ctx {
     uint64_t autoflush = 0;  // launch a group once it holds this many segments (0 = off)
     uint64_t seq = 0;        // segments queued so far (orders the groups of a flush)
     bool host_pointers = false;  // iov_base values are the caller's host addresses: resolve them
+    bool compact_rows = true;    // DRAID_EC_CTX_ROWS=64 turns compact rows off (A/B, tests)
     int fail_after = 0;      // test hook: the n-th piece from now fails before it launches
     // Flush tickets: an event recorded behind each ticketed flush, so a poller can
     // complete the requests of one flush while later ones are still running.
@@ -240,12 +252,12 @@ const uint32_t* address_order(draid_ec_ctx* c, const Group& g)
     return c->perm.data();
 }
 
-Group& group_for(draid_ec_ctx* c, int op, uint32_t k, uint32_t m)
+Group& group_for(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, bool compact)
 {
     for (Group& g : c->groups)
-        if (g.op == op && g.k == k && g.m == m && g.level == c->level)
+        if (g.op == op && g.k == k && g.m == m && g.level == c->level && g.compact == compact)
             return g;
-    c->groups.emplace_back(op, k, m, c->level);
+    c->groups.emplace_back(op, k, m, c->level, compact);
     return c->groups.back();
 }
 
@@ -324,18 +336,42 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             return ctx_arg("an iovec is neither memory of the context's GPU nor pinned / "
                            "registered host memory");
     }
-    Group& g = group_for(c, op, k, m);
-    if (const int rc = g.ready())
-        return rc;
-    const size_t n_ptrs = g.ptrs.size(), n_len = g.len.size(), n_fail = g.fail.size();
-    const uint64_t n_q = c->queued_segments;
+    // A run whose strips all lie within +-2 GiB of its first strip -- every run of
+    // an ordinary stripe -- is queued as a compact row; one that does not is queued
+    // as a row of pointers, in a group of its own ((op, k, m) groups carry no order
+    // among their segments, so splitting them by row format changes nothing).
+    struct Touched {
+        Group* g = nullptr;
+        size_t n_ptrs = 0, n_len = 0, n_fail = 0;
+    } touched[2];
+    int ready_rc = 0;
+    auto use = [&](bool compact) -> Group* {
+        Touched& t = touched[compact ? 1 : 0];
+        if (!t.g) {
+            Group& g = group_for(c, op, k, m, compact);
+            if ((ready_rc = g.ready()) != 0)
+                return nullptr;
+            t.g = &g;
+            t.n_ptrs = g.ptrs.size();
+            t.n_len = g.len.size();
+            t.n_fail = g.fail.size();
+        }
+        return t.g;
+    };
+    const uint64_t n_q = c->queued_segments, n_seq = c->seq;
     auto rollback = [&](const char* what) {  // a rejected stripe queues nothing
-        g.ptrs.shrink(n_ptrs);
-        g.len.resize(n_len);
-        g.fail.resize(n_fail);
+        for (Touched& t : touched)
+            if (t.g) {
+                t.g->ptrs.shrink(t.n_ptrs);
+                t.g->len.resize(t.n_len);
+                t.g->fail.resize(t.n_fail);
+            }
         c->queued_segments = n_q;
+        c->seq = n_seq;
         return ctx_arg(what);
     };
+    const bool may_compact = c->compact_rows && op != 2;
+    const uint8_t* ptr[512];
     size_t remaining = len;
     while (remaining > 0) {
         size_t run = std::min<size_t>(remaining, kMaxSegment);
@@ -375,15 +411,13 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             if (it[j].bad)
                 return rollback("an iovec is neither memory of the context's GPU nor pinned / "
                                 "registered host memory");
-        if (g.len.empty())
-            g.first_seq = c->seq;
-        ++c->seq;
-        const void** out = g.ptrs.grow(g.w);
-        if (!out)
-            return rollback("out of pinned host memory for descriptors");
+        // the run's strip addresses, and whether they fit a compact row
+        bool compact = may_compact;
         for (uint32_t j = 0; j < n; ++j) {
             IovIter& t = it[j];
-            out[j] = t.p + t.delta;
+            ptr[j] = t.p + t.delta;
+            const intptr_t d = ptr[j] - ptr[0];
+            compact &= d >= INT32_MIN && d <= INT32_MAX;
             if (run <= t.left) {
                 t.p += run;
                 t.left -= run;
@@ -397,23 +431,50 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             t.p += r;
             t.left -= r;
         }
-        g.len.push_back(static_cast<uint32_t>(run));
-        if (op == 1) {  // failure pair into the row's spare slot
-            uintptr_t f = 0;
-            memcpy(&f, meta, 2);
-            out[n] = reinterpret_cast<const void*>(f);
-        } else if (nmeta) {
-            g.fail.insert(g.fail.end(), meta, meta + nmeta);
+        Group* gp = use(compact);
+        if (!gp) {
+            const int rc = ready_rc;
+            (void)rollback("descriptor storage not ready");
+            return rc;
         }
+        Group& g = *gp;
+        if (g.len.empty())
+            g.first_seq = c->seq;
+        ++c->seq;
+        const void** out = g.ptrs.grow(g.w);
+        if (!out)
+            return rollback("out of pinned host memory for descriptors");
+        uintptr_t f = 0;
+        if (op == 1)
+            memcpy(&f, meta, 2);  // the failure pair rides behind the strips
+        if (compact) {
+            out[0] = ptr[0];
+            int32_t* off = reinterpret_cast<int32_t*>(out + 1);
+            for (uint32_t j = 0; j < n; ++j)
+                off[j] = static_cast<int32_t>(ptr[j] - ptr[0]);
+            if (op == 1)
+                off[n] = static_cast<int32_t>(f);
+        } else {
+            for (uint32_t j = 0; j < n; ++j)
+                out[j] = ptr[j];
+            if (op == 1)
+                out[n] = reinterpret_cast<const void*>(f);
+        }
+        g.len.push_back(static_cast<uint32_t>(run));
+        if (op != 1 && nmeta)
+            g.fail.insert(g.fail.end(), meta, meta + nmeta);
         ++c->queued_segments;
         remaining -= run;
     }
     // (a group behind a fence waits for the flush: its predecessors must launch first)
-    if (c->autoflush && g.level == 0 && g.len.size() >= c->autoflush) {
-        DeviceGuard on(c->device);
-        const int rc = flush_group(c, g);
-        recount(c);
-        return rc;
+    for (Touched& t : touched) {
+        if (t.g && c->autoflush && t.g->level == 0 && t.g->len.size() >= c->autoflush) {
+            DeviceGuard on(c->device);
+            const int rc = flush_group(c, *t.g);
+            recount(c);
+            if (rc)
+                return rc;
+        }
     }
     return 0;
 }
@@ -528,14 +589,15 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     const auto* lens = reinterpret_cast<const uint32_t*>(d + o_len);
     const void* wl = uniform ? nullptr : d + o_work;
     const uint32_t ulen = lenp[0];
+    const uint32_t row_bytes = g.compact ? static_cast<uint32_t>(w * sizeof(void*)) : 0u;
+    // the failure pair's place in a row: behind the k + m pointers, or offsets
+    const size_t o_pair = g.compact ? 8 + 4 * static_cast<size_t>(n) : n * sizeof(void*);
     if (g.op == 0)
-        e = draid::launch_encode_work(g.k, g.m, tab, lens, wl, ulen, nwork, c->stream);
+        e = draid::launch_encode_work(g.k, g.m, tab, row_bytes, lens, wl, ulen, nwork, c->stream);
     else if (g.op == 1)
-        e = draid::launch_reconstruct_work(g.k, g.m, tab, w, lens,
-                                           d + o_ptr + n * sizeof(void*),
+        e = draid::launch_reconstruct_work(g.k, g.m, tab, w, row_bytes, lens, d + o_ptr + o_pair,
                                            static_cast<uint32_t>(w * sizeof(void*)), wl, ulen,
-                                           nwork,
-                                           c->stream);
+                                           nwork, c->stream);
     else
         e = draid::launch_update_work(g.m, g.k / 2, tab, d + o_fail, lens, wl, ulen, nwork,
                                       c->stream);
@@ -557,14 +619,22 @@ int flush_single(draid_ec_ctx* c, Group& g)
     draid::ArgPtrTable args;
     memset(&args, 0, sizeof(args));
     const uint32_t n = g.k + g.m;
-    for (uint32_t j = 0; j < n; ++j)
-        args.p[j] = static_cast<const uint8_t*>(g.ptrs[j]);
+    const uint8_t* row = reinterpret_cast<const uint8_t*>(g.ptrs.data());
+    for (uint32_t j = 0; j < n; ++j) {
+        if (g.compact) {
+            int32_t off;
+            memcpy(&off, row + 8 + 4 * j, sizeof(off));
+            args.p[j] = static_cast<const uint8_t*>(g.ptrs[0]) + off;
+        } else {
+            args.p[j] = static_cast<const uint8_t*>(g.ptrs[j]);
+        }
+    }
     hipError_t e;
     if (g.op == 0)
         e = draid::launch_encode(g.k, g.m, g.len[0], 1, nullptr, &args, c->stream);
     else {
-        uint8_t f[sizeof(void*)];
-        memcpy(f, &g.ptrs.data()[n], sizeof(f));  // the row's failure-pair slot
+        uint8_t f[4];
+        memcpy(f, row + (g.compact ? 8 + 4 * n : n * sizeof(void*)), sizeof(f));  // the pair's slot
         e = draid::launch_reconstruct(g.k, g.m, g.len[0], 1, nullptr, &args, nullptr, f[0], f[1],
                                       nullptr, c->stream);
     }
@@ -654,6 +724,9 @@ int draid_ec_ctx_create(draid_ec_ctx** out)
     draid_ec_ctx* c = new (std::nothrow) draid_ec_ctx();
     if (!c)
         return ctx_arg("out of host memory");
+    const char* rows = getenv("DRAID_EC_CTX_ROWS");
+    if (rows && strcmp(rows, "64") == 0)
+        c->compact_rows = false;
     const char* order = getenv("DRAID_EC_CTX_ADDRESS_ORDER");
     if (order && (order[0] == '0' || order[0] == '2'))
         c->address_order = order[0] - '0';

@@ -602,38 +602,65 @@ static WorkSrc work_src(const uint32_t* seg_len, const void* work, uint32_t ulen
     return ws;
 }
 
+// row_bytes != 0: the table holds compact rows (RowOffs) that far apart instead of
+// rows of 64-bit pointers.
 template <int KT, int M, class C>
-static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, const uint32_t* seg_len,
-                                 const void* work, uint32_t ulen, uint32_t nwork, hipStream_t st)
+static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, uint32_t row_bytes,
+                                 const uint32_t* seg_len, const void* work, uint32_t ulen,
+                                 uint32_t nwork, hipStream_t st)
 {
     if (nwork == 0)
         return hipSuccess;
-    if constexpr (C::SPLIT > 1)
-        hipLaunchKernelGGL((k_encode_work_split<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                           TablePtrs{tab, k + M}, work_src<C>(seg_len, work, ulen), nwork);
-    else
-        hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                           WorkEncPtrs<KT>{tab, k + M}, k, work_src<C>(seg_len, work, ulen),
-                           nwork);
+    const RowOffs rows{reinterpret_cast<const uint8_t*>(tab), row_bytes};
+    if constexpr (C::SPLIT > 1) {
+        if (row_bytes)
+            hipLaunchKernelGGL((k_encode_work_split<KT, M, C, RowOffs>), dim3(nwork),
+                               dim3(C::NTHR), 0, st, rows, work_src<C>(seg_len, work, ulen),
+                               nwork);
+        else
+            hipLaunchKernelGGL((k_encode_work_split<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                               TablePtrs{tab, k + M}, work_src<C>(seg_len, work, ulen), nwork);
+    } else {
+        if (row_bytes)
+            hipLaunchKernelGGL((k_encode_work<KT, M, false, C, RowOffs>), dim3(nwork),
+                               dim3(C::NTHR), 0, st, rows, k, work_src<C>(seg_len, work, ulen),
+                               nwork);
+        else
+            hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0,
+                               st, WorkEncPtrs<KT>{tab, k + M}, k,
+                               work_src<C>(seg_len, work, ulen), nwork);
+    }
     return hipGetLastError();
 }
 
 template <int KT, int M, class C>
 static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t tstride, uint32_t k,
-                                      const uint32_t* seg_len, const uint8_t* fail,
-                                      uint32_t fstride, const void* work, uint32_t ulen,
-                                      uint32_t nwork, hipStream_t st)
+                                      uint32_t row_bytes, const uint32_t* seg_len,
+                                      const uint8_t* fail, uint32_t fstride, const void* work,
+                                      uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
     if (nwork == 0)
         return hipSuccess;
-    if constexpr (C::SPLIT > 1)
-        hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                           TablePtrs{tab, tstride}, work_src<C>(seg_len, work, ulen), fail,
-                           fstride, nwork);
-    else
-        hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
-                           TablePtrs{tab, tstride}, k, work_src<C>(seg_len, work, ulen), fail,
-                           fstride, nwork);
+    const RowOffs rows{reinterpret_cast<const uint8_t*>(tab), row_bytes};
+    if constexpr (C::SPLIT > 1) {
+        if (row_bytes)
+            hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C, RowOffs>), dim3(nwork),
+                               dim3(C::NTHR), 0, st, rows, work_src<C>(seg_len, work, ulen), fail,
+                               fstride, nwork);
+        else
+            hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0,
+                               st, TablePtrs{tab, tstride}, work_src<C>(seg_len, work, ulen), fail,
+                               fstride, nwork);
+    } else {
+        if (row_bytes)
+            hipLaunchKernelGGL((k_reconstruct_work<KT, M, C, RowOffs>), dim3(nwork), dim3(C::NTHR),
+                               0, st, rows, k, work_src<C>(seg_len, work, ulen), fail, fstride,
+                               nwork);
+        else
+            hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+                               TablePtrs{tab, tstride}, k, work_src<C>(seg_len, work, ulen), fail,
+                               fstride, nwork);
+    }
     return hipGetLastError();
 }
 
@@ -656,26 +683,26 @@ uint32_t work_chunk_bytes(int op, uint32_t k)
 }
 
 hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,
-                              const uint32_t* seg_len, const void* work, uint32_t ulen,
-                              uint32_t nwork, hipStream_t st)
+                              uint32_t row_bytes, const uint32_t* seg_len, const void* work,
+                              uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
     switch (k) {
 #define DRAID_CASE(K)                                                                        \
     case K:                                                                                  \
         return m == 1 ? go_encode_work<K, 1, EncCfg<enc_unroll(K), 0, enc_split_waves(K, 1),  \
                                                     enc_split(K)>>(                          \
-                            table, k, seg_len, work, ulen, nwork, st)                        \
+                            table, k, row_bytes, seg_len, work, ulen, nwork, st)             \
                       : go_encode_work<K, 2, EncCfg<enc_unroll(K), 0, enc_split_waves(K, 2),  \
                                                     enc_split(K)>>(                          \
-                            table, k, seg_len, work, ulen, nwork, st);
+                            table, k, row_bytes, seg_len, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
         return m == 1
-                   ? go_encode_work<0, 1, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(table, k, seg_len, work,
-                                                                            ulen, nwork, st)
-                   : go_encode_work<0, 2, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(table, k, seg_len, work,
-                                                                            ulen, nwork, st);
+                   ? go_encode_work<0, 1, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(
+                         table, k, row_bytes, seg_len, work, ulen, nwork, st)
+                   : go_encode_work<0, 2, EncCfg<1, 0, DRAID_RT_ENC_WAVES>>(
+                         table, k, row_bytes, seg_len, work, ulen, nwork, st);
     }
 }
 
@@ -689,26 +716,26 @@ hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* tabl
 #define DRAID_REC_WORK_WAVES(K, M) \
     (DRAID_REC_WORK_COLS ? rec_split_waves(K, M) : rec_waves(K, M))
 hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
-                                   uint32_t tstride, const uint32_t* seg_len, const uint8_t* fail,
-                                   uint32_t fstride, const void* work, uint32_t ulen,
-                                   uint32_t nwork, hipStream_t st)
+                                   uint32_t tstride, uint32_t row_bytes, const uint32_t* seg_len,
+                                   const uint8_t* fail, uint32_t fstride, const void* work,
+                                   uint32_t ulen, uint32_t nwork, hipStream_t st)
 {
     switch (k) {
 #define DRAID_CASE(K)                                                                         \
     case K:                                                                                   \
         return m == 1 ? go_reconstruct_work<K, 1, RecCfg<1, DRAID_REC_WORK_WAVES(K, 1),             \
                                                          DRAID_REC_WORK_SPLIT(K)>>(             \
-                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st) \
+                            table, tstride, k, row_bytes, seg_len, fail, fstride, work, ulen, nwork, st) \
                       : go_reconstruct_work<K, 2, RecCfg<1, DRAID_REC_WORK_WAVES(K, 2),             \
                                                          DRAID_REC_WORK_SPLIT(K)>>(             \
-                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
+                            table, tstride, k, row_bytes, seg_len, fail, fstride, work, ulen, nwork, st);
         DRAID_FOR_EACH_K(DRAID_CASE)
 #undef DRAID_CASE
     default:
         return m == 1 ? go_reconstruct_work<0, 1, RecCfg<1, DRAID_RT_REC_WAVES>>(
-                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st)
+                            table, tstride, k, row_bytes, seg_len, fail, fstride, work, ulen, nwork, st)
                       : go_reconstruct_work<0, 2, RecCfg<1, DRAID_RT_REC_WAVES>>(
-                            table, tstride, k, seg_len, fail, fstride, work, ulen, nwork, st);
+                            table, tstride, k, row_bytes, seg_len, fail, fstride, work, ulen, nwork, st);
     }
 }
 

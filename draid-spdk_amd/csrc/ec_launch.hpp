@@ -67,15 +67,18 @@ uint32_t work_chunk_bytes(int op, uint32_t k);
 // work == nullptr: every segment is `ulen` bytes and item b is chunk
 // b % cps of segment b / cps (cps = ceil(ulen / work_chunk_bytes)); seg_len
 // is then unused.
+// row_bytes == 0: `table` holds one row of 64-bit strip pointers per segment.
+// row_bytes != 0: compact rows, row_bytes apart -- an 8-byte base pointer, then
+// the int32 offset of every strip from it (then anything).
 hipError_t launch_encode_work(uint32_t k, uint32_t m, const uint8_t* const* table,
-                              const uint32_t* seg_len, const void* work, uint32_t ulen,
-                              uint32_t nwork, hipStream_t stream);
-// Reconstruct rows are `tstride` pointers wide (k + m strips, then anything);
-// segment s's failure pair is fail[fstride * s], fail[fstride * s + 1].
+                              uint32_t row_bytes, const uint32_t* seg_len, const void* work,
+                              uint32_t ulen, uint32_t nwork, hipStream_t stream);
+// Reconstruct rows of pointers are `tstride` pointers wide (k + m strips, then
+// anything); segment s's failure pair is fail[fstride * s], fail[fstride * s + 1].
 hipError_t launch_reconstruct_work(uint32_t k, uint32_t m, const uint8_t* const* table,
-                                   uint32_t tstride, const uint32_t* seg_len, const uint8_t* fail,
-                                   uint32_t fstride, const void* work, uint32_t ulen,
-                                   uint32_t nwork, hipStream_t stream);
+                                   uint32_t tstride, uint32_t row_bytes, const uint32_t* seg_len,
+                                   const uint8_t* fail, uint32_t fstride, const void* work,
+                                   uint32_t ulen, uint32_t nwork, hipStream_t stream);
 
 // Read-modify-write parity update over a segment work list (op 2): table rows
 // [O_0, N_0, ..., O_{nd-1}, N_{nd-1}, P, (Q)], exps rows sorted descending.

@@ -66,6 +66,28 @@ struct StridedPtrs {
     }
 };
 
+// Compact rows of the scatter-gather lists (ec_ctx.cpp): segment s is
+//   [8-byte base pointer][int32 offset of strip 0, 1, ... from it][anything]
+// row_bytes apart -- a little over half the bytes of a row of 64-bit pointers,
+// which is what a batch of short runs spends its PCIe upload on.  Read through the
+// constant address space like the pointer table: scalar loads, the strip base in
+// SGPRs.
+struct RowOffs {
+    const uint8_t* rows;
+    uint32_t row_bytes;
+    __device__ __forceinline__ const uint8_t* get(uint32_t s, int j) const
+    {
+        typedef const uint8_t* const __attribute__((address_space(4)))* cbase;
+        typedef const int32_t __attribute__((address_space(4)))* coff;
+        const uintptr_t row = reinterpret_cast<uintptr_t>(rows) + static_cast<size_t>(s) * row_bytes;
+        const uint8_t* p = ((cbase)row)[0] + ((coff)(row + 8))[j];
+#if DRAID_KEEP_POINTERS
+        asm("" : "+s"(p));
+#endif
+        return p;
+    }
+};
+
 struct ArgPtrs {
     ArgPtrTable t;
     __device__ __forceinline__ const uint8_t* get(uint32_t, int j) const { return t.p[j]; }

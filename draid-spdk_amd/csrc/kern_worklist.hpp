@@ -60,9 +60,9 @@ struct WorkSrc {
 template <int KT>
 using WorkEncPtrs = std::conditional_t<(KT > 0), TablePlain, TablePtrs>;
 
-template <int KT, int M, bool CHECK, class C>
+template <int KT, int M, bool CHECK, class C, class P = WorkEncPtrs<KT>>
 __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(
-    WorkEncPtrs<KT> pp, uint32_t k_rt, WorkSrc ws, uint32_t nwork)
+    P pp, uint32_t k_rt, WorkSrc ws, uint32_t nwork)
 {
     constexpr uint32_t CB = static_cast<uint32_t>(C::NTHR) * C::U * 16;
     const int k = KT > 0 ? KT : static_cast<int>(k_rt);
@@ -74,9 +74,9 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work(
 }
 
 // The shared-item encode over a segment list: one workgroup per work item.
-template <int KT, int M, class C>
+template <int KT, int M, class C, class P = TablePtrs>
 __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work_split(
-    TablePtrs pp, WorkSrc ws, uint32_t nwork)
+    P pp, WorkSrc ws, uint32_t nwork)
 {
     static_assert(KT > 0 && C::SPLIT > 1, "shared items need a compile-time width");
     constexpr uint32_t CB = static_cast<uint32_t>(C::ITEM) * C::U * 16;
@@ -86,8 +86,8 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_encode_work_s
     encode_item_split<KT, M, false, C>(pp, seg, chunk, len, cps, lds);
 }
 
-template <int KT, int M, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_work(TablePtrs pp, uint32_t k_rt,
+template <int KT, int M, class C, class P = TablePtrs>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_work(P pp, uint32_t k_rt,
                                                               WorkSrc ws, const uint8_t* fail,
                                                               uint32_t fstride, uint32_t nwork)
 {
@@ -119,9 +119,9 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_w
 
 // The column reconstruct over a segment list: one workgroup per work item.  The
 // failure pair rides at a row stride beside the segment's pointers.
-template <int KT, int M, class C>
+template <int KT, int M, class C, class P = TablePtrs>
 __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_reconstruct_work_cols(
-    TablePtrs pp, WorkSrc ws, const uint8_t* fail, uint32_t fstride, uint32_t nwork)
+    P pp, WorkSrc ws, const uint8_t* fail, uint32_t fstride, uint32_t nwork)
 {
     static_assert(KT > 0 && C::SPLIT > 1, "shared items need a compile-time width");
     constexpr uint32_t CB = static_cast<uint32_t>(C::ITEM) * C::U * 16;

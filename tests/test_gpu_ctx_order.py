@@ -69,8 +69,9 @@ def test_groups_run_in_queue_order_of_the_current_batch(ec):
 def test_failed_flush_keeps_exactly_the_unlaunched_segments(ec):
     k, m, L, B = 16, 2, 256, 15000
     n = k + m
-    piece = max(4096, (1 << 20) // (n * 8 + 12))  # segments per ~1 MiB descriptor piece
-    assert 2 * piece < B < 3 * piece               # three pieces
+    row = (8 + 4 * n + 7) // 8 * 8                 # a compact row: base pointer + int32 offsets
+    piece = max(4096, (1 << 20) // (row + 12))     # segments per ~1 MiB descriptor piece
+    assert piece < B < 2 * piece                   # two pieces
     a, ref = stripes(k, m, L, B, 2)
     d = torch.from_numpy(a).to(DEV)
     torch.cuda.synchronize()

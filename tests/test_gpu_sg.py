@@ -578,3 +578,71 @@ def test_sg_mark_and_rollback_drop_exactly_one_request(ec):
     assert oracle.encode_strided(ref.reshape(-1), k, m, L, 3, L, n * L) == 0
     assert (got[0] == ref[0]).all() and (got[2] == ref[2]).all()
     assert (got[1] == before[1]).all(), "the rolled-back request touched its buffers"
+
+
+def test_sg_rows_compact_and_wide(ec, monkeypatch):
+    """The context queues a run as a compact row (base pointer + 32-bit offsets) when
+    its strips lie within 2 GiB of the first one, and as a row of 64-bit pointers when
+    they do not; both kinds may share a batch.  Stripes whose strips sit at both ends
+    of a 2.6 GiB buffer (wide rows) are queued between ordinary ones (compact rows),
+    encoded and rebuilt; then the whole batch again with compact rows switched off
+    (DRAID_EC_CTX_ROWS=64), which must give the same bytes."""
+    k, m, L, B = 5, 2, 4096 + 16, 12
+    n = k + m
+    far = (1 << 31) + (300 << 20)                     # > 2 GiB
+    big = torch.zeros(far + B * n * L + 4096, dtype=torch.uint8, device=DEV)
+    rng = np.random.default_rng(99)
+    data = rng.integers(0, 256, (B, n, L), dtype=np.uint8)
+    data[:, k:] = 0
+    ref = data.copy()
+    assert oracle.encode_strided(ref.reshape(-1), k, m, L, B, L, n * L) == 0
+    base = big.data_ptr()
+
+    def where(s, j):      # odd stripes: strips 1, 3, ... live 2.3 GiB above the others
+        off = (s * n + j) * L
+        return off + (far if (s % 2 == 1 and j % 2 == 1) else 0)
+
+    def strips(s):
+        return [[(base + where(s, j), L)] for j in range(n)]
+
+    def put(vals):
+        for s in range(B):
+            for j in range(n):
+                o = where(s, j)
+                big[o:o + L] = torch.from_numpy(vals[s, j]).to(DEV)
+
+    def get():
+        out = np.zeros((B, n, L), np.uint8)
+        for s in range(B):
+            for j in range(n):
+                o = where(s, j)
+                out[s, j] = big[o:o + L].cpu().numpy()
+        return out
+
+    for rows in (None, "64"):
+        if rows:
+            monkeypatch.setenv("DRAID_EC_CTX_ROWS", rows)     # read at ctx creation
+        put(data)
+        torch.cuda.synchronize()
+        ctx = ec.Ctx()
+        try:
+            for s in range(B):
+                ctx.encode_sg(k, m, strips(s), L)
+            assert ctx.queued() == B
+            ctx.flush()
+            ctx.synchronize()
+            assert (get() == ref).all(), rows
+            fails = [[(s + 1) % k, k + (s % 2)] for s in range(B)]   # a data strip and P or Q
+            erased = ref.copy()
+            for s in range(B):
+                for f in fails[s]:
+                    erased[s, f] = 0x3C
+            put(erased)
+            torch.cuda.synchronize()
+            for s in range(B):
+                ctx.reconstruct_sg(k, m, strips(s), L, fails[s])
+            ctx.flush()
+            ctx.synchronize()
+            assert (get() == ref).all(), rows
+        finally:
+            ctx.close()
