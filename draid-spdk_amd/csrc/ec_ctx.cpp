@@ -372,6 +372,9 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     };
     const bool may_compact = c->compact_rows && op != 2;
     const uint8_t* ptr[512];
+    uintptr_t fpair = 0;
+    if (op == 1)
+        memcpy(&fpair, meta, 2);
     size_t remaining = len;
     while (remaining > 0) {
         size_t run = std::min<size_t>(remaining, kMaxSegment);
@@ -407,59 +410,73 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             }
             run = std::min<size_t>(run, avail);
         }
-        for (uint32_t j = 0; j < n; ++j)
-            if (it[j].bad)
-                return rollback("an iovec is neither memory of the context's GPU nor pinned / "
-                                "registered host memory");
-        // the run's strip addresses, and whether they fit a compact row
-        bool compact = may_compact;
-        for (uint32_t j = 0; j < n; ++j) {
-            IovIter& t = it[j];
-            ptr[j] = t.p + t.delta;
-            const intptr_t d = ptr[j] - ptr[0];
-            compact &= d >= INT32_MIN && d <= INT32_MAX;
-            if (run <= t.left) {
-                t.p += run;
-                t.left -= run;
-                continue;
-            }
-            size_t r = run;  // crossed merged iovecs
-            while (r > t.left) {
-                r -= t.left;
-                t.enter(t.idx + 1);
-            }
-            t.p += r;
-            t.left -= r;
-        }
-        Group* gp = use(compact);
+        // One pass writes the run's row and moves every strip's iterator on.  The row
+        // is written as a compact one where those are allowed, and redone as a row of
+        // pointers in the rare run that turns out not to fit.
+        Group* gp = use(may_compact);
         if (!gp) {
             const int rc = ready_rc;
             (void)rollback("descriptor storage not ready");
             return rc;
         }
+        const void** out = gp->ptrs.grow(gp->w);
+        if (!out)
+            return rollback("out of pinned host memory for descriptors");
+        const uint8_t* const p0 = it[0].p + it[0].delta;
+        int32_t* const off = reinterpret_cast<int32_t*>(out + 1);
+        bool fits = true, bad = false;
+        for (uint32_t j = 0; j < n; ++j) {
+            IovIter& t = it[j];
+            const uint8_t* const pj = t.p + t.delta;
+            ptr[j] = pj;
+            if (may_compact) {
+                const intptr_t d = pj - p0;
+                off[j] = static_cast<int32_t>(d);
+                fits &= d == static_cast<int32_t>(d);
+            } else {
+                out[j] = pj;
+            }
+            if (run <= t.left) {
+                t.p += run;
+                t.left -= run;
+            } else {
+                size_t r = run;  // crossed merged iovecs
+                while (r > t.left) {
+                    r -= t.left;
+                    t.enter(t.idx + 1);
+                }
+                t.p += r;
+                t.left -= r;
+            }
+            bad |= t.bad;
+        }
+        if (bad)
+            return rollback("an iovec is neither memory of the context's GPU nor pinned / "
+                            "registered host memory");
+        if (may_compact && fits) {
+            out[0] = p0;
+            if (op == 1)
+                off[n] = static_cast<int32_t>(fpair);  // the failure pair rides behind the strips
+        } else {
+            if (may_compact) {  // strips more than 2 GiB apart: a row of pointers after all
+                gp->ptrs.shrink(gp->ptrs.size() - gp->w);
+                if (!(gp = use(false))) {
+                    const int rc = ready_rc;
+                    (void)rollback("descriptor storage not ready");
+                    return rc;
+                }
+                if (!(out = gp->ptrs.grow(gp->w)))
+                    return rollback("out of pinned host memory for descriptors");
+                for (uint32_t j = 0; j < n; ++j)
+                    out[j] = ptr[j];
+            }
+            if (op == 1)
+                out[n] = reinterpret_cast<const void*>(fpair);
+        }
         Group& g = *gp;
         if (g.len.empty())
             g.first_seq = c->seq;
         ++c->seq;
-        const void** out = g.ptrs.grow(g.w);
-        if (!out)
-            return rollback("out of pinned host memory for descriptors");
-        uintptr_t f = 0;
-        if (op == 1)
-            memcpy(&f, meta, 2);  // the failure pair rides behind the strips
-        if (compact) {
-            out[0] = ptr[0];
-            int32_t* off = reinterpret_cast<int32_t*>(out + 1);
-            for (uint32_t j = 0; j < n; ++j)
-                off[j] = static_cast<int32_t>(ptr[j] - ptr[0]);
-            if (op == 1)
-                off[n] = static_cast<int32_t>(f);
-        } else {
-            for (uint32_t j = 0; j < n; ++j)
-                out[j] = ptr[j];
-            if (op == 1)
-                out[n] = reinterpret_cast<const void*>(f);
-        }
         g.len.push_back(static_cast<uint32_t>(run));
         if (op != 1 && nmeta)
             g.fail.insert(g.fail.end(), meta, meta + nmeta);

@@ -10,18 +10,23 @@
 //   D+P / D+D recovery                            gf_vect_mul.c:242-347
 //
 // Shape: a work item is one 1 KiB chunk of every strip of one stripe (64 lanes x
-// one 16-byte vector per strip).  Three workgroup shapes run items (the launch
+// one 16-byte vector per strip).  Four workgroup shapes run items (the launch
 // policy below picks one per width, by measurement):
 //   - one 64-lane wave per item, loading all k strips (k_encode, k_reconstruct):
-//     k = 2, the RAID6 reconstruct up to k = 7, run-time widths above 20;
+//     k = 2, the RAID6 reconstruct up to k = 7 (2+2 and 4+2 with two vectors per
+//     lane), and the run-time widths: above 32, and above 20 outside the
+//     batched calls;
 //   - an item shared by 2 or 4 waves that deal the strips among themselves, each
 //     accumulating P and the Horner form of Q over its own strips, the parts
 //     combined through LDS after one barrier (k_encode_split): every encode
-//     from k = 3;
+//     from k = 3 to 32;
 //   - an item shared by two waves that deal the loads by strip and the
 //     arithmetic by column: raw vectors to LDS rows, one barrier, then every lane
 //     runs both syndromes down its own columns (k_reconstruct_cols): the
-//     reconstruct from k = 8.
+//     reconstruct from k = 8 to 20;
+//   - the reconstruct dealt by strip like the encode, four waves per item
+//     (k_reconstruct_split): k = 21 to 32, where the column shape's (k + 2) KiB of
+//     LDS per item leave a CU too few items.
 // With k known at compile time every strip load of a wave is issued before its
 // first XOR.  HBM is the roofline: encode moves (k+m)*S algorithmic bytes per
 // stripe and does ~2 VALU ops per byte read, far below the VALU ceiling.
@@ -264,10 +269,11 @@ constexpr int rec_waves(int k, int m)
 //                stores) loses or ties at every shape: 8+2 x 64 KiB 399-406 vs 388 us,
 //                4+1 202-211 vs 196, 12+2 282-288 vs 278, 16+2 x 256 KiB 379 vs 379.
 //   reconstruct  dealing the arithmetic by strip as the encode does costs it too much
-//                (failure decode and plan in every wave, the scaling of the Q parts):
-//                with four waves only k = 16 won (380 vs 399), 14+2 (349 vs 341),
-//                12+2 (330 vs 305) and 8+2 dual (447 vs 420) lost; that kernel is no
-//                longer in the source.  Dealing only the
+//                below k = 21 (failure decode and plan in every wave, the scaling of the
+//                Q parts): with four waves only k = 16 won (380 vs 399), 14+2 (349 vs
+//                341), 12+2 (330 vs 305) and 8+2 dual (447 vs 420) lost, and 17..20 lose
+//                4-6% against the columns (18+2 443 vs 425); from k = 21 up it wins
+//                (k_reconstruct_split, rec_by_strip below).  Dealing only the
 //                LOADS by strip and the arithmetic by column (k_reconstruct_cols), two
 //                waves per item, wins from k = 8 up against the one-wave kernel at its
 //                best occupancy: 8+1 365.6 vs 376.7, 10+2 480 vs 494, 12+2 288 vs 298.7,
@@ -313,8 +319,11 @@ constexpr int enc_split_waves(int k, int m)
 {
     return DRAID_ENC_WAVES >= 0 ? DRAID_ENC_WAVES
            : enc_split(k) == 1  ? enc_waves(k)
-           : (k == 8 && m == 2) ? 7
+           : (k >= 8 && k <= 10 && m == 2) ? 7  // 9+2 399 vs 408-418 us at 6, 10+2 392 vs 396.5
            : (m == 1 && (k == 4 || k == 5)) ? 5
+           : (k == 24 || k >= 27) ? 4  // 24+2 385 vs 389 us at 5, 29+2 393.5 vs 400, 32+2 376 vs
+                                       // 380, 24+1 392 vs 398, 27+1 397 vs 402; 22+2 405 vs 394.5
+                                       // and 26+2 397 vs 393 the other way, 21, 23, 25 the same
            : k >= 17            ? 5  // 18+2 394-396 vs 398-399 us at 6, 403 at 7
                                 : 6;
 }
