@@ -110,6 +110,17 @@ def test_module_on_four_spdk_threads_and_through_hot_remove():
 
 
 @pytest.mark.gpu
+def test_module_on_four_spdk_threads_over_several_device_slots():
+    """The same four-thread run with three device slots per channel (DRAID_RAID_GPUS=3, all
+    on the one GPU): every channel owns three contexts, a stripe's slot is s mod 3 whatever
+    thread its request came from, and each slot has its own launches in flight."""
+    out = run("spdk_raid_threads_test", env={"DRAID_RAID_GPUS": "3"})
+    assert "ok interleaved: 4 SPDK threads" in out
+    assert out.count("ok OS threads: 4 pthreads") == 2
+    assert "ok hot-remove, reference behaviour: array offline" in out
+
+
+@pytest.mark.gpu
 def test_hot_remove_with_the_redirect_keeps_the_array_online():
     out = run("spdk_raid_hotremove_test")
     assert "ok hot-remove with the redirect: online through two removals, offline at the third" in out
