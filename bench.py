@@ -413,9 +413,9 @@ def main() -> None:
         ec.reconstruct(batch, fail, sh)
         ev[i][2].record(stream)
     torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()  # this rank's K steps; the job's time is the max over ranks below
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
 
     elapsed = t1 - t0
     enc_all = [e[0].elapsed_time(e[1]) for e in ev]

@@ -10,8 +10,9 @@
 // pointers, written straight into pinned memory, + a length).
 // draid_ec_ctx_flush() DMAs the queued descriptors of each (op, k, m) group in
 // pieces of about 1 MiB on a copy stream and launches one kernel per piece on
-// the compute stream, so uploads overlap kernels.  A context is single-threaded, like an
-// SPDK io_channel: one per reactor thread.
+// the compute stream, so uploads overlap kernels; pieces of small segments are
+// uploaded already while the batch is still being queued (stage_ahead).  A context is
+// single-threaded, like an SPDK io_channel: one per reactor thread.
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -28,7 +29,10 @@
 
 namespace {
 
-constexpr int kSlots = 8;
+constexpr int kSlots = 16;
+// Pieces a context may hold uploaded but not yet launched (below): the other
+// slots stay free for the pieces a flush packs itself.
+constexpr int kMaxStaged = 12;
 constexpr size_t kPieceBytes = 1u << 20;       // descriptors per launch (≈ 1 MiB)
 constexpr size_t kMinPieceSegments = 4096;
 constexpr uint64_t kMaxSegment = 1ull << 30;
@@ -50,6 +54,7 @@ public:
     const void* operator[](size_t i) const { return p_[i]; }
     void clear() { n_ = 0; }
     void shrink(size_t n) { n_ = std::min(n_, n); }
+    bool full(size_t add) const { return n_ + add > cap_; }  // grow(add) would move the array
     // Appends `add` uninitialised elements; null when pinned memory runs out.
     const void** grow(size_t add)
     {
@@ -61,7 +66,7 @@ public:
             if (n_)
                 memcpy(q, p_, n_ * sizeof(void*));
             if (p_)
-                (void)hipHostFree(p_);  // never in flight: see Group::ready()
+                (void)hipHostFree(p_);  // never in flight: see Group::ready() and walk()
             p_ = static_cast<const void**>(q);
             cap_ = cap;
         }
@@ -83,6 +88,16 @@ constexpr uint32_t row_slots(int op, uint32_t n, bool compact)
 {
     return compact ? (8u + 4u * n + (op == 1 ? 4u : 0u) + 7u) / 8u : n + (op == 1 ? 1u : 0u);
 }
+
+// A piece of a group whose descriptors are in a ring slot and on their way to
+// the device (or there already); only its launch is left.
+struct Staged {
+    int slot = -1;
+    size_t s0 = 0, s1 = 0;          // the group's segments [s0, s1)
+    bool uniform = false;           // every segment the same length: no work list
+    uint32_t nwork = 0, ulen = 0;   // work items; the uniform length
+    size_t o_len = 0, o_fail = 0, o_work = 0;  // offsets into the slot
+};
 
 struct Group {
     Group(int op_, uint32_t k_, uint32_t m_, uint32_t level_, bool compact_)
@@ -115,7 +130,12 @@ struct Group {
     PinnedPtrs spare;
     hipEvent_t uploaded[2] = {nullptr, nullptr};  // [0] for ptrs, [1] for spare
     bool pending[2] = {false, false};
-    bool direct = false;  // this flush DMA'd from ptrs
+    bool direct = false;  // copies of this batch DMA'd from ptrs
+    // Pieces uploaded from inside the queueing calls, ahead of the flush (see
+    // stage_ahead): always the batch's leading segments [0, staged_upto), in order.
+    std::vector<Staged> staged;
+    size_t staged_upto = 0;
+    uint64_t tail_bytes = 0;  // sum of len over the segments from staged_upto on
 
     int ready()  // before writing into ptrs
     {
@@ -134,6 +154,7 @@ struct Slot {
     hipEvent_t done = nullptr;      // the piece's kernel finished (slot reusable)
     hipEvent_t uploaded = nullptr;  // the piece's descriptors are on the device
     bool used = false;
+    bool staged = false;            // holds a piece that has not launched yet: not to be reused
 };
 
 int ctx_fail(hipError_t e, const char* what) { return draid::fail_hip(e, what); }
@@ -150,6 +171,8 @@ struct draid_ec_ctx {
     std::deque<Group> groups;  // deque: groups never move (pinned storage, events)
     Slot slots[kSlots];
     int next = 0;
+    int staged_slots = 0;    // slots holding uploaded pieces that wait for their launch
+    bool stage_ahead = true; // DRAID_EC_CTX_STAGE_AHEAD=0 turns the early uploads off (A/B, tests)
     uint64_t queued_segments = 0;
     int address_order = 1;  // DRAID_EC_CTX_ADDRESS_ORDER: 0 off, 1 auto, 2 any out-of-order group
                             // (diagnostics and tests)
@@ -315,6 +338,8 @@ bool iter_seek(IovIter& it, size_t offset)
 }
 
 int flush_group(draid_ec_ctx* c, Group& g);
+size_t piece_segments(const Group& g);
+int stage_ahead(draid_ec_ctx* c, Group& g);
 
 // The walk of raid5_xor_stripe: runs of n = min over strips of the bytes left
 // in each strip's current iovec; one descriptor per run.
@@ -343,6 +368,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     struct Touched {
         Group* g = nullptr;
         size_t n_ptrs = 0, n_len = 0, n_fail = 0;
+        uint64_t tail_bytes = 0;
     } touched[2];
     int ready_rc = 0;
     auto use = [&](bool compact) -> Group* {
@@ -355,6 +381,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             t.n_ptrs = g.ptrs.size();
             t.n_len = g.len.size();
             t.n_fail = g.fail.size();
+            t.tail_bytes = g.tail_bytes;
         }
         return t.g;
     };
@@ -365,6 +392,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                 t.g->ptrs.shrink(t.n_ptrs);
                 t.g->len.resize(t.n_len);
                 t.g->fail.resize(t.n_fail);
+                t.g->tail_bytes = t.tail_bytes;
             }
         c->queued_segments = n_q;
         c->seq = n_seq;
@@ -419,6 +447,9 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             (void)rollback("descriptor storage not ready");
             return rc;
         }
+        // (growing moves the rows: no early upload may still be reading them)
+        if (gp->direct && gp->ptrs.full(gp->w))
+            (void)hipStreamSynchronize(c->copy);
         const void** out = gp->ptrs.grow(gp->w);
         if (!out)
             return rollback("out of pinned host memory for descriptors");
@@ -465,6 +496,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                     (void)rollback("descriptor storage not ready");
                     return rc;
                 }
+                if (gp->direct && gp->ptrs.full(gp->w))
+                    (void)hipStreamSynchronize(c->copy);
                 if (!(out = gp->ptrs.grow(gp->w)))
                     return rollback("out of pinned host memory for descriptors");
                 for (uint32_t j = 0; j < n; ++j)
@@ -478,6 +511,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             g.first_seq = c->seq;
         ++c->seq;
         g.len.push_back(static_cast<uint32_t>(run));
+        g.tail_bytes += run;
         if (op != 1 && nmeta)
             g.fail.insert(g.fail.end(), meta, meta + nmeta);
         ++c->queued_segments;
@@ -491,22 +525,51 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             recount(c);
             if (rc)
                 return rc;
+        } else if (t.g && c->stage_ahead && t.g->len.size() - t.g->staged_upto >= piece_segments(*t.g)) {
+            DeviceGuard on(c->device);
+            const int rc = stage_ahead(c, *t.g);
+            if (rc)
+                return rc;
         }
     }
     return 0;
 }
 
-// One launch over segments [s0, s1) of a group: pack their descriptors into the
-// next pinned ring slot, DMA them on the copy stream, and launch on the compute
-// stream once the copy has landed.  Copies therefore overlap the kernels of
-// earlier pieces and flushes.
-// `perm` (may be null): segment i of the group is g's segment perm[i].
-int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size_t s1)
+constexpr int kSlotBusy = 0x7fff;  // stage_piece(ahead): not an error, nothing staged
+
+// Segments of a group per launch: about kPieceBytes of descriptors.
+size_t piece_segments(const Group& g)
 {
-    if (c->fail_after > 0 && --c->fail_after == 0)
-        return ctx_fail(hipErrorOutOfMemory, "flush piece (injected failure)");
+    const size_t per_seg = g.w * sizeof(void*) + sizeof(uint32_t) + 2 * sizeof(uint32_t);
+    return std::max<size_t>(kMinPieceSegments, kPieceBytes / per_seg);
+}
+
+// Forgets the staged pieces that reach beyond segment `keep` (their slots are
+// free again; copies still in flight into them are harmless, the copy stream
+// runs the next upload into the same slot behind them).
+void drop_staged(draid_ec_ctx* c, Group& g, size_t keep)
+{
+    while (!g.staged.empty() && g.staged.back().s1 > keep) {
+        c->slots[g.staged.back().slot].staged = false;
+        --c->staged_slots;
+        g.staged.pop_back();
+    }
+    g.staged_upto = g.staged.empty() ? 0 : g.staged.back().s1;
+    uint64_t tail = 0;
+    for (size_t s = g.staged_upto; s < g.len.size(); ++s)
+        tail += g.len[s];
+    g.tail_bytes = tail;
+}
+
+// First half of a launch over segments [s0, s1) of a group: pack their
+// descriptors into the next pinned ring slot and DMA them on the copy stream.
+// `perm` (may be null): segment i of the group is g's segment perm[i].
+// `ahead`: called from a queueing call -- never waits for a slot still in use
+// (returns 1 and stages nothing).
+int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size_t s1, bool ahead,
+                Staged* out)
+{
     const size_t nseg = s1 - s0;
-    const uint32_t n = g.k + g.m;
     const size_t nmeta = g.fail.size() / g.len.size();  // bytes of meta per segment
     const uint32_t cb = draid::work_chunk_bytes(g.op, g.k);
     std::vector<uint32_t> plen;
@@ -536,7 +599,6 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     }
     if (nwork64 > 0x7fffffffull)
         return ctx_arg("flush: too many work items queued (flush more often)");
-    const uint32_t nwork = static_cast<uint32_t>(nwork64);
     const size_t o_ptr = 0;
     const uint32_t w = g.w;
     const size_t o_len = align8(o_ptr + nseg * w * sizeof(void*));
@@ -544,14 +606,26 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     const size_t o_work = align8(o_fail + nseg * nmeta);
     const size_t bytes = o_work + work.size() * sizeof(uint32_t);
 
-    Slot& sl = c->slots[c->next];
-    c->next = (c->next + 1) % kSlots;
+    // the next slot that holds no piece waiting for its launch (at least
+    // kSlots - kMaxStaged of them never do)
+    int si = c->next;
+    while (c->slots[si].staged)
+        si = (si + 1) % kSlots;
+    Slot& sl = c->slots[si];
     hipError_t e;
     if (sl.used) {  // back-pressure: the slot's previous upload+launch must be done
-        e = hipEventSynchronize(sl.done);
+        if (ahead) {
+            if ((e = hipEventQuery(sl.done)) == hipErrorNotReady) {
+                (void)hipGetLastError();
+                return kSlotBusy;
+            }
+        } else {
+            e = hipEventSynchronize(sl.done);
+        }
         if (e != hipSuccess)
             return ctx_fail(e, "hipEventSynchronize(slot)");
     }
+    c->next = (si + 1) % kSlots;
     if (sl.cap < bytes) {
         if (sl.host)
             (void)hipHostFree(sl.host);
@@ -598,31 +672,85 @@ int flush_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     }
     if (e != hipSuccess)
         return ctx_fail(e, "hipMemcpyAsync(descriptors)");
-    if ((e = hipEventRecord(sl.uploaded, c->copy)) != hipSuccess ||
-        (e = hipStreamWaitEvent(c->stream, sl.uploaded, 0)) != hipSuccess)
+    if ((e = hipEventRecord(sl.uploaded, c->copy)) != hipSuccess)
+        return ctx_fail(e, "descriptor upload event");
+    out->slot = si;
+    out->s0 = s0;
+    out->s1 = s1;
+    out->uniform = uniform;
+    out->nwork = static_cast<uint32_t>(nwork64);
+    out->ulen = lenp[0];
+    out->o_len = o_len;
+    out->o_fail = o_fail;
+    out->o_work = o_work;
+    return 0;
+}
+
+// Second half: the piece's kernel on the compute stream, behind its upload.
+// Copies therefore overlap the kernels of earlier pieces and flushes.
+int launch_piece(draid_ec_ctx* c, Group& g, const Staged& st)
+{
+    Slot& sl = c->slots[st.slot];
+    const uint32_t n = g.k + g.m, w = g.w;
+    hipError_t e;
+    if ((e = hipStreamWaitEvent(c->stream, sl.uploaded, 0)) != hipSuccess)
         return ctx_fail(e, "descriptor upload event");
     const uint8_t* d = static_cast<const uint8_t*>(sl.dev);
-    const auto* tab = reinterpret_cast<const uint8_t* const*>(d + o_ptr);
-    const auto* lens = reinterpret_cast<const uint32_t*>(d + o_len);
-    const void* wl = uniform ? nullptr : d + o_work;
-    const uint32_t ulen = lenp[0];
+    const auto* tab = reinterpret_cast<const uint8_t* const*>(d);
+    const auto* lens = reinterpret_cast<const uint32_t*>(d + st.o_len);
+    const void* wl = st.uniform ? nullptr : d + st.o_work;
     const uint32_t row_bytes = g.compact ? static_cast<uint32_t>(w * sizeof(void*)) : 0u;
     // the failure pair's place in a row: behind the k + m pointers, or offsets
     const size_t o_pair = g.compact ? 8 + 4 * static_cast<size_t>(n) : n * sizeof(void*);
     if (g.op == 0)
-        e = draid::launch_encode_work(g.k, g.m, tab, row_bytes, lens, wl, ulen, nwork, c->stream);
-    else if (g.op == 1)
-        e = draid::launch_reconstruct_work(g.k, g.m, tab, w, row_bytes, lens, d + o_ptr + o_pair,
-                                           static_cast<uint32_t>(w * sizeof(void*)), wl, ulen,
-                                           nwork, c->stream);
-    else
-        e = draid::launch_update_work(g.m, g.k / 2, tab, d + o_fail, lens, wl, ulen, nwork,
+        e = draid::launch_encode_work(g.k, g.m, tab, row_bytes, lens, wl, st.ulen, st.nwork,
                                       c->stream);
+    else if (g.op == 1)
+        e = draid::launch_reconstruct_work(g.k, g.m, tab, w, row_bytes, lens, d + o_pair,
+                                           static_cast<uint32_t>(w * sizeof(void*)), wl, st.ulen,
+                                           st.nwork, c->stream);
+    else
+        e = draid::launch_update_work(g.m, g.k / 2, tab, d + st.o_fail, lens, wl, st.ulen,
+                                      st.nwork, c->stream);
     if (e != hipSuccess)
         return ctx_fail(e, "launch (segment work list)");
     if ((e = hipEventRecord(sl.done, c->stream)) != hipSuccess)
         return ctx_fail(e, "hipEventRecord(slot)");
     sl.used = true;
+    return 0;
+}
+
+// Descriptors ahead of the flush.  A batch of small runs carries a lot of
+// descriptor bytes per strip byte (4 KiB iovecs: 3 MiB per 4096 stripes), and a
+// flush that starts uploading them only when it is called leaves the GPU waiting
+// for the first piece.  So once a group holds a whole piece of segments that no
+// flush will reorder (small ones), the queueing call that completes the piece
+// uploads it there and then; the flush finds it on the device and only launches.
+// A piece is final when it is uploaded: segments are only ever appended, and a
+// rollback that cuts into a staged piece drops it (drop_staged).
+int stage_ahead(draid_ec_ctx* c, Group& g)
+{
+    const size_t piece = piece_segments(g);
+    const uint32_t n = g.k + g.m;
+    while (g.len.size() - g.staged_upto >= piece && c->staged_slots < kMaxStaged) {
+        const size_t tail = g.len.size() - g.staged_upto;
+        if (g.tail_bytes * n >= kOrderMinSegmentBytes * tail)
+            break;  // large segments: few descriptors, and the flush may sort them
+        Staged st;
+        const int rc = stage_piece(c, g, nullptr, g.staged_upto, g.staged_upto + piece, true, &st);
+        if (rc == kSlotBusy)
+            break;  // the next free slot is still in flight: the flush will do it
+        if (rc)
+            return rc;
+        uint64_t bytes = 0;
+        for (size_t s = st.s0; s < st.s1; ++s)
+            bytes += g.len[s];
+        g.tail_bytes -= bytes;
+        c->slots[st.slot].staged = true;
+        ++c->staged_slots;
+        g.staged.push_back(st);
+        g.staged_upto = st.s1;
+    }
     return 0;
 }
 
@@ -658,6 +786,7 @@ int flush_single(draid_ec_ctx* c, Group& g)
     g.ptrs.clear();
     g.len.clear();
     g.fail.clear();
+    g.tail_bytes = 0;
     return e == hipSuccess ? 0 : ctx_fail(e, "launch (single segment)");
 }
 
@@ -669,18 +798,30 @@ int flush_group(draid_ec_ctx* c, Group& g)
     ++c->launches;
     if (nseg == 1 && g.op != 2 && g.k + g.m <= static_cast<uint32_t>(draid::kMaxArgPtrs))
         return flush_single(c, g);
-    const size_t per_seg = g.w * sizeof(void*) + sizeof(uint32_t) + 2 * sizeof(uint32_t);
-    const size_t piece = std::max<size_t>(kMinPieceSegments, kPieceBytes / per_seg);
-    const uint32_t* perm = address_order(c, g);
+    const size_t piece = piece_segments(g);
+    // (a batch with pieces on the device already keeps its queue order)
+    const uint32_t* perm = g.staged.empty() ? address_order(c, g) : nullptr;
     int rc = 0;
-    g.direct = false;
     size_t launched = 0;
-    for (size_t s0 = 0; s0 < nseg; s0 += piece) {
-        rc = flush_piece(c, g, perm, s0, std::min(nseg, s0 + piece));
-        if (rc)
+    auto injected = [&]() {  // test hook: this piece fails before it launches
+        return c->fail_after > 0 && --c->fail_after == 0
+                   ? ctx_fail(hipErrorOutOfMemory, "flush piece (injected failure)")
+                   : 0;
+    };
+    for (const Staged& st : g.staged) {
+        if ((rc = injected()) != 0 || (rc = launch_piece(c, g, st)) != 0)
             break;
-        launched = std::min(nseg, s0 + piece);
+        launched = st.s1;
     }
+    for (size_t s0 = g.staged_upto; rc == 0 && s0 < nseg; s0 += piece) {
+        Staged st;
+        if ((rc = injected()) != 0 ||
+            (rc = stage_piece(c, g, perm, s0, std::min(nseg, s0 + piece), false, &st)) != 0 ||
+            (rc = launch_piece(c, g, st)) != 0)
+            break;
+        launched = st.s1;
+    }
+    drop_staged(c, g, 0);  // launched, or (on failure) queued again below
     if (rc && launched < nseg) {
         // A piece failed (descriptor memory, the work-item limit, a launch error):
         // the pieces before it are running, this one and the rest are not.  Keep
@@ -688,6 +829,7 @@ int flush_group(draid_ec_ctx* c, Group& g)
         // flush again or fail precisely the requests that did not run.
         (void)hipStreamSynchronize(c->copy);  // nothing may still read g.ptrs
         g.pending[0] = g.pending[1] = false;
+        g.direct = false;
         std::vector<uint32_t> rest;
         rest.reserve(nseg - launched);
         for (size_t i = launched; i < nseg; ++i)
@@ -695,16 +837,19 @@ int flush_group(draid_ec_ctx* c, Group& g)
         std::sort(rest.begin(), rest.end());
         const size_t nmeta = g.fail.size() / nseg;
         const void** rows = g.ptrs.data();
+        uint64_t tail = 0;
         for (size_t i = 0; i < rest.size(); ++i) {  // rest[i] >= i: forward moves are safe
             memmove(rows + i * g.w, rows + static_cast<size_t>(rest[i]) * g.w,
                     g.w * sizeof(void*));
             g.len[i] = g.len[rest[i]];
+            tail += g.len[i];
             if (nmeta)
                 memmove(g.fail.data() + i * nmeta, g.fail.data() + rest[i] * nmeta, nmeta);
         }
         g.ptrs.shrink(rest.size() * g.w);
         g.len.resize(rest.size());
         g.fail.resize(rest.size() * nmeta);
+        g.tail_bytes = tail;
         return rc;
     }
     if (g.direct) {  // copies from g.ptrs in flight: walk the next batch into the spare
@@ -723,10 +868,12 @@ int flush_group(draid_ec_ctx* c, Group& g)
         g.ptrs.swap(g.spare);
         std::swap(g.uploaded[0], g.uploaded[1]);
         std::swap(g.pending[0], g.pending[1]);
+        g.direct = false;
     }
     g.ptrs.clear();
     g.len.clear();
     g.fail.clear();
+    g.tail_bytes = 0;
     return rc;
 }
 
@@ -747,6 +894,10 @@ int draid_ec_ctx_create(draid_ec_ctx** out)
     const char* order = getenv("DRAID_EC_CTX_ADDRESS_ORDER");
     if (order && (order[0] == '0' || order[0] == '2'))
         c->address_order = order[0] - '0';
+    const char* ahead = getenv("DRAID_EC_CTX_STAGE_AHEAD");
+    // (a context told to sort every group cannot upload pieces in queue order)
+    if ((ahead && ahead[0] == '0') || c->address_order == 2)
+        c->stage_ahead = false;
     hipError_t e = hipGetDevice(&c->device);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -956,6 +1107,10 @@ void draid_ec_ctx_test_fail_after(draid_ec_ctx* c, int n)
         c->fail_after = n;
 }
 
+// Test hook (not in the public header): pieces uploaded ahead of the flush that
+// wait for their launch.
+int draid_ec_ctx_test_staged(draid_ec_ctx* c) { return c ? c->staged_slots : 0; }
+
 int draid_ec_ctx_query(draid_ec_ctx* c)
 {
     if (!c)
@@ -985,10 +1140,13 @@ int draid_ec_ctx_discard_queued(draid_ec_ctx* c)
     if (!c)
         return ctx_arg("ctx is NULL");
     for (Group& g : c->groups) {
-        if (g.ready())  // the storage may still feed an earlier flush's copies
-            (void)hipStreamSynchronize(c->copy);
-        g.ptrs.clear();
         g.len.clear();
+        drop_staged(c, g, 0);
+        // the storage may still feed an earlier flush's copies, or this batch's early ones
+        if (g.ready() || g.direct)
+            (void)hipStreamSynchronize(c->copy);
+        g.direct = false;
+        g.ptrs.clear();
         g.fail.clear();
     }
     c->queued_segments = 0;
@@ -1038,6 +1196,7 @@ int draid_ec_ctx_rollback(draid_ec_ctx* c)
         g.ptrs.shrink(keep * g.w);
         g.len.resize(keep);
         g.fail.resize(keep * nmeta);
+        drop_staged(c, g, keep);  // a piece uploaded early that held any of them
     }
     c->seq = c->mark_seq;
     c->level = 0;

@@ -163,6 +163,8 @@ def lib() -> C.CDLL:
         L.draid_ec_ctx_set_host_pointers.argtypes = [vp, i32]
         L.draid_ec_ctx_test_fail_after.argtypes = [vp, i32]
         L.draid_ec_ctx_test_fail_after.restype = None
+        L.draid_ec_ctx_test_staged.argtypes = [vp]
+        L.draid_ec_ctx_test_staged.restype = i32
         L.draid_ec_ctx_encode_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t]
         L.draid_ec_ctx_reconstruct_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp,
                                                   C.c_size_t, i32, vp]
@@ -426,6 +428,10 @@ class Ctx:
     def test_fail_after(self, n: int):
         """Test hook: the n-th descriptor piece launched from now on fails."""
         lib().draid_ec_ctx_test_fail_after(self.h, n)
+
+    def test_staged(self) -> int:
+        """Test hook: descriptor pieces uploaded ahead of the flush, not yet launched."""
+        return lib().draid_ec_ctx_test_staged(self.h)
 
     def set_autoflush(self, segments: int):
         return _check(lib().draid_ec_ctx_set_autoflush(self.h, segments), "ctx_set_autoflush")

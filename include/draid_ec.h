@@ -206,7 +206,11 @@ void *draid_ec_ctx_stream(draid_ec_ctx *ctx);
  * descriptors into pinned memory.  They can wait -- for the descriptor upload of
  * the flush before last, when a group is queued into again while those copies
  * still run -- and they allocate pinned memory when a group outgrows its
- * descriptor storage (it doubles, from 1 MiB). */
+ * descriptor storage (it doubles, from 1 MiB).  A call that completes a ~1 MiB
+ * piece of descriptors of small segments (under 128 KiB of strips each) also
+ * starts that piece's upload, so a flush of many small runs finds most of its
+ * descriptors on the device (at most 12 pieces wait like that; the call never
+ * waits for a ring slot; DRAID_EC_CTX_STAGE_AHEAD=0 turns it off). */
 int draid_ec_ctx_encode_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m,
                            const struct iovec *const *iovs, const int *iovcnt,
                            const size_t *offset, size_t len);
@@ -229,8 +233,8 @@ int draid_ec_ctx_update_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m, uint32_t n
                            const int *par_cnt, size_t len);
 
 /* Launch everything queued.  Non-blocking, except that each ~1 MiB piece of
- * descriptors takes one of 8 ring slots and waits for that slot's previous
- * kernel when all 8 are in flight (and allocates the slot's buffers on first
+ * descriptors takes one of 16 ring slots and waits for that slot's previous
+ * kernel when all 16 are in flight (and allocates the slot's buffers on first
  * use or growth).  The context's stream is non-blocking: it does not wait for
  * work on other streams, so every queued buffer must hold its data when flush
  * is called.

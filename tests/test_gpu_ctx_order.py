@@ -201,3 +201,150 @@ def test_context_resolves_host_pointers_of_pinned_memory(ec):
         assert ctx.queued() == 0
     finally:
         ctx.close()
+
+
+# ---- descriptor pieces uploaded ahead of the flush ----
+#
+# A group of small segments uploads each ~1 MiB piece of descriptors from inside
+# the queueing call that completes it; the flush then only launches those pieces.
+# What must hold: the same bytes as with flush-time uploads, for uniform and mixed
+# segment lengths; a rollback or discard that cuts into an uploaded piece drops it.
+
+def _piece(k, m, reconstruct=False):
+    row = (8 + 4 * (k + m) + (4 if reconstruct else 0) + 7) // 8 * 8
+    return max(4096, (1 << 20) // (row + 12))
+
+
+@pytest.mark.parametrize("ahead", [True, False])
+def test_early_uploads_same_bytes_as_flush_time_uploads(ec, ahead, monkeypatch):
+    if not ahead:
+        monkeypatch.setenv("DRAID_EC_CTX_STAGE_AHEAD", "0")
+    k, m, L = 8, 2, 256
+    n = k + m
+    piece = _piece(k, m)
+    B = 2 * piece + 1500                      # two whole pieces ahead, a third at the flush
+    a, ref = stripes(k, m, L, B, 11)
+    d = torch.from_numpy(a).to(DEV)
+    torch.cuda.synchronize()
+    ctx = ec.Ctx()
+    try:
+        seen = 0
+        for s in range(B):
+            ctx.encode_sg(k, m, runs(d, s, n), L)
+            seen = max(seen, ctx.test_staged())
+        assert seen == (2 if ahead else 0)
+        assert ctx.queued() == B
+        ctx.flush()
+        ctx.synchronize()
+        assert ctx.test_staged() == 0 and ctx.queued() == 0
+        assert (d.cpu().numpy() == ref).all()
+        # mixed lengths (a work list per piece): even stripes in one run, odd ones in two halves
+        d[:, 1].zero_()
+        d[:, 6].zero_()
+        torch.cuda.synchronize()
+        h = L // 2
+        seen = 0
+        for s in range(B):
+            if s % 2 == 0:
+                ctx.reconstruct_sg(k, m, runs(d, s, n), L, [6, 1])
+            else:
+                for off in (0, h):
+                    ctx.reconstruct_sg(k, m, [[(d[s, j].data_ptr() + off, h)] for j in range(n)],
+                                       h, [1, 6])
+            seen = max(seen, ctx.test_staged())
+        assert seen >= (2 if ahead else 0) and (ahead or seen == 0)
+        ctx.flush()
+        ctx.synchronize()
+        assert (d.cpu().numpy() == ref).all()
+    finally:
+        ctx.close()
+
+
+def test_rollback_and_discard_drop_early_uploads(ec):
+    k, m, L = 8, 2, 256
+    n = k + m
+    piece = _piece(k, m)
+    B = piece + 600
+    a, ref = stripes(k, m, L, B, 12)
+    d = torch.from_numpy(a).to(DEV)
+    torch.cuda.synchronize()
+    ctx = ec.Ctx()
+    try:
+        # a request's mark sits inside the first piece; the piece is uploaded while the
+        # request is still queueing; the request then fails and is rolled back
+        for s in range(piece - 300):
+            ctx.encode_sg(k, m, runs(d, s, n), L)
+        ctx.mark()
+        for s in range(piece - 300, piece + 100):
+            ctx.encode_sg(k, m, runs(d, s, n), L)
+        assert ctx.test_staged() == 1
+        ctx.rollback()
+        assert ctx.test_staged() == 0 and ctx.queued() == piece - 300
+        # other stripes take the rolled-back rows: [piece - 300, piece) stays unencoded
+        for s in range(piece, B):
+            ctx.encode_sg(k, m, runs(d, s, n), L)
+        assert ctx.test_staged() == 1          # (piece - 300) + 600 segments: a new first piece
+        ctx.flush()
+        ctx.synchronize()
+        got = d.cpu().numpy()
+        skipped = slice(piece - 300, piece)
+        assert not got[skipped, k:].any(), "a rolled-back segment ran"
+        assert (got[:piece - 300] == ref[:piece - 300]).all() and (got[piece:] == ref[piece:]).all()
+        # discard: a whole uploaded piece is forgotten, nothing of it runs
+        d2 = torch.from_numpy(a).to(DEV)
+        torch.cuda.synchronize()
+        for s in range(B):
+            ctx.encode_sg(k, m, runs(d2, s, n), L)
+        assert ctx.test_staged() == 1
+        assert ec.lib().draid_ec_ctx_discard_queued(ctx.h) == 0
+        assert ctx.test_staged() == 0 and ctx.queued() == 0
+        ctx.flush()
+        ctx.synchronize()
+        assert not d2[:, k:].any().item(), "a discarded segment ran"
+        for s in range(B):
+            ctx.encode_sg(k, m, runs(d2, s, n), L)
+        ctx.flush()
+        ctx.synchronize()
+        assert (d2.cpu().numpy() == ref).all()
+    finally:
+        ctx.close()
+
+
+def test_early_uploads_leave_slots_for_other_groups(ec):
+    """More small segments than the context may hold uploaded ahead, then a second
+    group in the same flush: the flush packs what is left into the free slots."""
+    k, m, L = 2, 1, 64
+    n = k + m
+    piece = _piece(k, m)
+    B = 14 * piece + 10                          # more pieces than may wait uploaded (12)
+    a, ref = stripes(k, m, L, B, 13)
+    d = torch.from_numpy(a).to(DEV)
+    k2, m2, L2, B2 = 4, 2, 2048, 40
+    a2, ref2 = stripes(k2, m2, L2, B2, 14)
+    d2 = torch.from_numpy(a2).to(DEV)
+    torch.cuda.synchronize()
+    ctx = ec.Ctx()
+    try:
+        lib, h = ec.lib(), ctx.h
+        import ctypes as C
+        # (queued through one reused argument block: 57k stripes in a Python loop)
+        iov = (ec.IoVec * n)()
+        heads = (C.c_void_p * n)(*[C.addressof(iov) + j * C.sizeof(ec.IoVec) for j in range(n)])
+        cnts = (C.c_int * n)(*([1] * n))
+        base = d.data_ptr()
+        for j in range(n):
+            iov[j].iov_len = L
+        for s in range(B):
+            for j in range(n):
+                iov[j].iov_base = base + (s * n + j) * L
+            assert lib.draid_ec_ctx_encode_sg(h, k, m, heads, cnts, None, L) == 0
+        assert ctx.test_staged() == 12
+        for s in range(B2):
+            ctx.encode_sg(k2, m2, runs(d2, s, k2 + m2), L2)
+        ctx.flush()
+        ctx.synchronize()
+        assert ctx.test_staged() == 0
+        assert (d.cpu().numpy() == ref).all()
+        assert (d2.cpu().numpy() == ref2).all()
+    finally:
+        ctx.close()

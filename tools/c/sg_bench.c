@@ -97,7 +97,7 @@ int main(int argc, char **argv)
     for (int op = 0; op < 3; ++op) {
         double walk = 0, flush = 0, wall = 0;
         float gpu = 0;
-        for (int r = -8; r < reps; ++r) { /* warm-ups fill all 8 descriptor slots */
+        for (int r = -16; r < reps; ++r) { /* warm-ups fill all 16 descriptor slots */
             CHECK(draid_ec_ctx_synchronize(ctx));
             double t0 = now();
             /* With autoflush the queueing calls launch kernels themselves, so the

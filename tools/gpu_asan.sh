@@ -20,6 +20,10 @@ DRAID_EC_CTX_ADDRESS_ORDER=2 timeout -k 10 120 tests/c/sg_bench_asan_gpu 1024 64
 # without autoflush (the next batch walked while earlier copies are in flight)
 timeout -k 10 120 tests/c/sg_bench_asan_gpu 1024 256 3 0 >> $L 2>&1 || { tail -40 $L; exit 1; }
 timeout -k 10 120 tests/c/sg_bench_asan_gpu 4096 512 3 0 1024 >> $L 2>&1 || { tail -40 $L; exit 1; }
+# enough small segments for descriptor pieces uploaded ahead of the flush (three per
+# batch at 1 KiB iovecs x 1024 stripes), alone and with autoflush launching between them
+timeout -k 10 180 tests/c/sg_bench_asan_gpu 1024 1024 2 0 >> $L 2>&1 || { tail -40 $L; exit 1; }
+timeout -k 10 180 tests/c/sg_bench_asan_gpu 1024 1024 2 0 30000 >> $L 2>&1 || { tail -40 $L; exit 1; }
 grep -c "AddressSanitizer" $L && exit 1
 grep -c "^PASS" $L
 tail -12 $L
