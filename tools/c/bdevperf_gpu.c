@@ -137,8 +137,23 @@ int main(int argc, char **argv)
         memcpy(g_user_h + b, &x, 8);
     }
     memset(g_par_h, 0, g_par_len);
-    OK(draid_ec_host_register(g_user_h, g_user_len));
-    OK(draid_ec_host_register(g_par_h, g_par_len));
+    /* hosts whose GPU runtime refuses to register existing memory: the same buffers
+     * from the runtime's own pinned allocator instead (what a module does there) */
+    int registered = 1;
+    if (draid_ec_host_register(g_user_h, g_user_len) != 0) {
+        uint8_t *u = NULL, *p = NULL;
+        registered = 0;
+        OK(draid_ec_host_alloc((void **)&u, g_user_len));
+        OK(draid_ec_host_alloc((void **)&p, g_par_len));
+        memcpy(u, g_user_h, g_user_len);
+        memset(p, 0, g_par_len);
+        free(g_user_h);
+        free(g_par_h);
+        g_user_h = u;
+        g_par_h = p;
+    } else {
+        OK(draid_ec_host_register(g_par_h, g_par_len));
+    }
     OK(draid_ec_host_device_pointer(g_user_h, (void **)&g_user_d));
     OK(draid_ec_host_device_pointer(g_par_h, (void **)&g_par_d));
 
@@ -202,14 +217,20 @@ int main(int argc, char **argv)
     printf("{\"harness\": \"bdevperf_gpu\", \"config\": \"RAID5 4+1 full-stripe write, 64 KiB strip, "
            "5 RAM disks, parity on the GPU\", \"io_size\": %zu, \"qd\": %d, \"groups\": %d, "
            "\"seconds\": %.3f, \"ios\": %llu, \"mib_s\": %.1f, \"iops\": %.1f, \"polls\": %llu, "
-           "\"parity_verified\": %s, \"device_address_equals_host\": %s}\n",
+           "\"parity_verified\": %s, \"device_address_equals_host\": %s, \"buffers\": \"%s\"}\n",
            g_io_bytes, qd, groups, el, (unsigned long long)done,
            (double)done * (double)g_io_bytes / el / (1024.0 * 1024.0), (double)done / el,
            (unsigned long long)polls, ok ? "true" : "false",
-           g_user_d == g_user_h ? "true" : "false");
+           g_user_d == g_user_h ? "true" : "false",
+           registered ? "registered (hipHostRegister)" : "pinned allocator (hipHostMalloc)");
     for (int g = 0; g < groups; g++)
         draid_ec_ctx_destroy(ctx[g]);
-    draid_ec_host_unregister(g_user_h);
-    draid_ec_host_unregister(g_par_h);
+    if (registered) {
+        draid_ec_host_unregister(g_user_h);
+        draid_ec_host_unregister(g_par_h);
+    } else {
+        draid_ec_host_free(g_user_h);
+        draid_ec_host_free(g_par_h);
+    }
     return ok ? 0 : 1;
 }
