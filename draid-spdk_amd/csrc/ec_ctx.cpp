@@ -33,6 +33,9 @@ constexpr int kSlots = 16;
 // Pieces a context may hold uploaded but not yet launched (below): the other
 // slots stay free for the pieces a flush packs itself.
 constexpr int kMaxStaged = 12;
+// A launch of at most this many segments reads its descriptors where the host
+// wrote them, in pinned memory, instead of waiting for their upload (stage_piece).
+constexpr size_t kInplaceSegments = 256;
 constexpr size_t kPieceBytes = 1u << 20;       // descriptors per launch (≈ 1 MiB)
 constexpr size_t kMinPieceSegments = 4096;
 constexpr uint64_t kMaxSegment = 1ull << 30;
@@ -95,6 +98,8 @@ struct Staged {
     int slot = -1;
     size_t s0 = 0, s1 = 0;          // the group's segments [s0, s1)
     bool uniform = false;           // every segment the same length: no work list
+    bool inplace = false;           // the kernel reads the descriptors from the slot's pinned
+                                    // host memory: nothing was uploaded
     uint32_t nwork = 0, ulen = 0;   // work items; the uniform length
     size_t o_len = 0, o_fail = 0, o_work = 0;  // offsets into the slot
 };
@@ -149,6 +154,7 @@ struct Group {
 
 struct Slot {
     void* host = nullptr;  // pinned
+    void* host_dev = nullptr;  // the device's address of `host`
     void* dev = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;      // the piece's kernel finished (slot reusable)
@@ -173,6 +179,7 @@ struct draid_ec_ctx {
     int next = 0;
     int staged_slots = 0;    // slots holding uploaded pieces that wait for their launch
     bool stage_ahead = true; // DRAID_EC_CTX_STAGE_AHEAD=0 turns the early uploads off (A/B, tests)
+    size_t inplace_segments = kInplaceSegments;  // DRAID_EC_CTX_INPLACE_SEGMENTS (A/B, tests)
     uint64_t queued_segments = 0;
     int address_order = 1;  // DRAID_EC_CTX_ADDRESS_ORDER: 0 off, 1 auto, 2 any out-of-order group
                             // (diagnostics and tests)
@@ -631,16 +638,29 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
             (void)hipHostFree(sl.host);
         if (sl.dev)
             (void)hipFree(sl.dev);
-        sl.host = sl.dev = nullptr;
+        sl.host = sl.host_dev = sl.dev = nullptr;
         sl.cap = 0;
         const size_t cap = std::max<size_t>(bytes * 2, 64 * 1024);
         if ((e = hipHostMalloc(&sl.host, cap, hipHostMallocDefault)) != hipSuccess)
             return ctx_fail(e, "hipHostMalloc(descriptor ring)");
+        if ((e = hipHostGetDevicePointer(&sl.host_dev, sl.host, 0)) != hipSuccess)
+            return ctx_fail(e, "hipHostGetDevicePointer(descriptor ring)");
         if ((e = hipMalloc(&sl.dev, cap)) != hipSuccess)
             return ctx_fail(e, "hipMalloc(descriptor ring)");
         sl.cap = cap;
     }
     uint8_t* h = static_cast<uint8_t*>(sl.host);
+    // A small launch (a poller's batch of a few dozen requests) reads its
+    // descriptors in place: uploading a few KiB costs the host 20 us of runtime calls
+    // (copy, event, cross-stream wait) and the GPU as long again before the kernel may
+    // start, while the kernel's reads of pinned memory add a PCIe round trip per item,
+    // which a launch this small does not notice.  Large launches do (4096 stripes of
+    // 4 KiB runs: 1.39 vs 1.00 ms), so they upload.  Wall time of one flush of B
+    // 8+2 stripes at 64 KiB runs, in place vs uploaded: B = 2..32 21-25 vs 41-46 us,
+    // 64: 31 vs 46, 128: 42 vs 53, 256: 59-65 vs 74-75, 1024: encode 198 vs 177.
+    const bool inplace = !ahead && nseg <= c->inplace_segments;
+    if (inplace && !perm)
+        memcpy(h + o_ptr, g.ptrs.data() + s0 * w, nseg * w * sizeof(void*));
     if (perm) {
         auto* hp = reinterpret_cast<const void**>(h + o_ptr);
         for (size_t i = 0; i < nseg; ++i)
@@ -660,7 +680,9 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     // (Reading them in place from pinned memory instead was measured slower:
     // 1.39 vs 1.00 ms for 4096 stripes of 4 KiB iovecs -- the per-item pointer
     // loads then pay PCIe latency.)
-    if (perm)
+    if (inplace)
+        e = hipSuccess;
+    else if (perm)
         e = hipMemcpyAsync(sl.dev, sl.host, bytes, hipMemcpyHostToDevice, c->copy);
     else {
         e = hipMemcpyAsync(static_cast<uint8_t*>(sl.dev) + o_ptr, g.ptrs.data() + s0 * w,
@@ -672,8 +694,9 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     }
     if (e != hipSuccess)
         return ctx_fail(e, "hipMemcpyAsync(descriptors)");
-    if ((e = hipEventRecord(sl.uploaded, c->copy)) != hipSuccess)
+    if (!inplace && (e = hipEventRecord(sl.uploaded, c->copy)) != hipSuccess)
         return ctx_fail(e, "descriptor upload event");
+    out->inplace = inplace;
     out->slot = si;
     out->s0 = s0;
     out->s1 = s1;
@@ -693,9 +716,9 @@ int launch_piece(draid_ec_ctx* c, Group& g, const Staged& st)
     Slot& sl = c->slots[st.slot];
     const uint32_t n = g.k + g.m, w = g.w;
     hipError_t e;
-    if ((e = hipStreamWaitEvent(c->stream, sl.uploaded, 0)) != hipSuccess)
+    if (!st.inplace && (e = hipStreamWaitEvent(c->stream, sl.uploaded, 0)) != hipSuccess)
         return ctx_fail(e, "descriptor upload event");
-    const uint8_t* d = static_cast<const uint8_t*>(sl.dev);
+    const uint8_t* d = static_cast<const uint8_t*>(st.inplace ? sl.host_dev : sl.dev);
     const auto* tab = reinterpret_cast<const uint8_t* const*>(d);
     const auto* lens = reinterpret_cast<const uint32_t*>(d + st.o_len);
     const void* wl = st.uniform ? nullptr : d + st.o_work;
@@ -898,6 +921,8 @@ int draid_ec_ctx_create(draid_ec_ctx** out)
     // (a context told to sort every group cannot upload pieces in queue order)
     if ((ahead && ahead[0] == '0') || c->address_order == 2)
         c->stage_ahead = false;
+    if (const char* inplace = getenv("DRAID_EC_CTX_INPLACE_SEGMENTS"))
+        c->inplace_segments = strtoul(inplace, nullptr, 0);
     hipError_t e = hipGetDevice(&c->device);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

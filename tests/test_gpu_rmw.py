@@ -24,7 +24,10 @@ def _runs(rng, base, length, pieces):
 
 @pytest.mark.parametrize("k,m,L,B", [(4, 1, 4096, 6), (8, 2, 65536, 5), (16, 2, 8192, 4),
                                      (8, 2, 1000, 5)])
-def test_rmw_update_matches_reencode(ec, k, m, L, B):
+@pytest.mark.parametrize("uploaded", [False, True])
+def test_rmw_update_matches_reencode(ec, k, m, L, B, uploaded, monkeypatch):
+    if uploaded:  # descriptors uploaded first instead of read in place (small launches)
+        monkeypatch.setenv("DRAID_EC_CTX_INPLACE_SEGMENTS", "0")
     rng = np.random.default_rng(k * 100 + L)
     n = k + m
     host = np.zeros((B, n, L), np.uint8)

@@ -74,13 +74,18 @@ def _fill(pool, rng):
 @pytest.mark.parametrize("k,m,L,B,prefix", [(4, 1, 4096, 6, False), (8, 2, 8192 + 48, 5, True),
                                             (16, 2, 3000, 3, False), (11, 2, 777, 4, True)])
 @pytest.mark.parametrize("shuffled", [False, True])
-def test_sg_encode_and_reconstruct(ec, k, m, L, B, prefix, shuffled, monkeypatch):
+@pytest.mark.parametrize("uploaded", [False, True])
+def test_sg_encode_and_reconstruct(ec, k, m, L, B, prefix, shuffled, uploaded, monkeypatch):
     """shuffled: stripes queued out of address order and the context told to
     reorder every out-of-order group (ec_ctx.cpp address_order; by default only
     large scattered segments are) -- pointers, lengths and failure pairs must
-    travel together."""
+    travel together.  uploaded: a launch this small reads its descriptors in place
+    from pinned memory by default; the other way they are uploaded first, as every
+    large launch's are."""
     if shuffled:
         monkeypatch.setenv("DRAID_EC_CTX_ADDRESS_ORDER", "2")  # read at ctx creation
+    if uploaded:
+        monkeypatch.setenv("DRAID_EC_CTX_INPLACE_SEGMENTS", "0")
     rng = np.random.default_rng(k * L + B)
     pool = Pool(rng, k, m, L, B, prefix=prefix)
     _fill(pool, rng)
