@@ -63,5 +63,46 @@ def main():
         json.dump(out, f, indent=1)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def two_streams():
+    """Two launches of B stripes each: back to back on one stream, or side by side on
+    two -- does running them together hide the fixed cost of a launch?"""
+    import time
+    import torch
+    import draid_ec as ec
+    ec.lib()
+    k, m, S = 8, 2, 65536
+    n = k + m
+    dev = torch.device("cuda", 0)
+    Bmax = 128
+    host = torch.empty(2 * Bmax * n * S, dtype=torch.uint8).pin_memory()
+    host.view(2 * Bmax, n, S)[:, :k] = torch.randint(0, 256, (2 * Bmax, k, S), dtype=torch.uint8)
+    hbase = ec.device_pointer(host.data_ptr(), host.numel())
+    s1, s2 = ec.stream_create(), ec.stream_create()
+    for B in (8, 16, 32, 64):
+        batches = []
+        for half in range(2):
+            tab = hbase + (np.arange(B * n, dtype=np.int64) + half * Bmax * n) * S
+            table = torch.from_numpy(tab).to(dev)
+            batches.append((ec.make_batch(k, m, S, B, table), table))
+        torch.cuda.synchronize(dev)
+        res = {}
+        for mode in ("one_stream", "two_streams"):
+            ts = []
+            for r in range(45):
+                t0 = time.perf_counter()
+                ec.encode(batches[0][0], s1)
+                ec.encode(batches[1][0], s1 if mode == "one_stream" else s2)
+                ec.stream_synchronize(s1)
+                ec.stream_synchronize(s2)
+                ts.append(time.perf_counter() - t0)
+            res[mode] = round(float(np.median(ts[5:])) * 1e6, 1)
+        print(json.dumps({"stripes_per_launch": B, "launches": 2, **{f"{k_}_us": v for k_, v in res.items()}}),
+              flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "two":
+    two_streams()
