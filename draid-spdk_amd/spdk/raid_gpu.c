@@ -61,9 +61,14 @@
 #include "raid_gpu.h"
 
 /* Stripe requests in flight per channel (raid5_simple.c:14 keeps 128 with one
- * parity buffer each; here each owns n strip buffers). */
-#define RG_REQUESTS_DEFAULT 64
+ * parity buffer each, raid5.c:1508 512 without buffers; here each owns n strip
+ * buffers): 128, fewer where that many would pin more than RG_POOL_BYTES per
+ * channel, never fewer than 32.  A launch carries up to half of them, and over
+ * PCIe every launch costs about 40 us whatever its size, so larger is faster. */
+#define RG_REQUESTS_DEFAULT 128
+#define RG_REQUESTS_MIN 32
 #define RG_REQUESTS_MAX 512
+#define RG_POOL_BYTES (256ull << 20)
 #define RG_MAX_GPUS 8
 /* Launches a channel keeps in flight per GPU.  While that many run, what the
  * reactor queues waits for the next poll instead of being launched in ever
@@ -306,9 +311,11 @@ static void _rg_start_request(void *ctx)
 	rg_start_request(ctx);
 }
 
+static void rg_submit(struct raid_bdev_io *raid_io, bool waited);
+
 static void _rg_resubmit(void *ctx)
 {
-	rg_submit_rw_request(ctx);
+	rg_submit(ctx, true);
 }
 
 /* raid5_complete_stripe_request (raid5.c:485-521): complete the parent I/O, hand
@@ -342,15 +349,21 @@ rg_complete(struct rg_request *req, enum spdk_bdev_io_status status)
 	req->raid_io = NULL;
 	TAILQ_INSERT_HEAD(&ch->free_reqs, req, link);
 	ch->busy_reqs--;
+	/* The freed request goes to the parent I/O that has waited longest, before the
+	 * completion below lets the caller submit a new one (a bdevperf-style caller
+	 * resubmits from its completion callback and would take the request every
+	 * time, leaving the waiting I/O where it is for as long as the load lasts). */
+	while (!TAILQ_EMPTY(&ch->free_reqs) && (wqe = TAILQ_FIRST(&ch->waiting)) != NULL) {
+		TAILQ_REMOVE(&ch->waiting, wqe, link);
+		wqe->cb_fn(wqe->cb_arg);
+		if (TAILQ_FIRST(&ch->waiting) == wqe) {
+			break;	/* back at the head: it waits for a stripe, not for a request */
+		}
+	}
 	{
 		RG_TIC(t_c);
 		raid_bdev_io_complete(raid_io, status);
 		RG_TOC(t_c, complete);
-	}
-	wqe = TAILQ_FIRST(&ch->waiting);
-	if (wqe) {
-		TAILQ_REMOVE(&ch->waiting, wqe, link);
-		wqe->cb_fn(wqe->cb_arg);
 	}
 }
 
@@ -761,6 +774,13 @@ rg_start_request(struct rg_request *req)
 static void
 rg_submit_rw_request(struct raid_bdev_io *raid_io)
 {
+	rg_submit(raid_io, false);
+}
+
+/* waited: the parent I/O comes from the head of the channel's waiting list. */
+static void
+rg_submit(struct raid_bdev_io *raid_io, bool waited)
+{
 	struct spdk_bdev_io *bdev_io = spdk_bdev_io_from_ctx(raid_io);
 	struct rg_channel *ch = raid_bdev_io_channel_get_resource(raid_io->raid_ch);
 	struct rg_info *info = ch->info;	/* module_private is gone once the module stopped */
@@ -774,14 +794,19 @@ rg_submit_rw_request(struct raid_bdev_io *raid_io)
 		return;
 	}
 	req = TAILQ_FIRST(&ch->free_reqs);
-	if (spdk_unlikely(req == NULL)) {
+	if (spdk_unlikely(req == NULL || (!waited && !TAILQ_EMPTY(&ch->waiting)))) {
 		/* all stripe requests in flight: retry when one completes
-		 * (raid5_simple.c:364-370) */
+		 * (raid5_simple.c:364-370).  Parent I/O of one channel gets its requests in
+		 * the order it was submitted: a new one queues behind those that wait. */
 		struct spdk_bdev_io_wait_entry *wqe = &raid_io->waitq_entry;
 
 		wqe->cb_fn = _rg_resubmit;
 		wqe->cb_arg = raid_io;
-		TAILQ_INSERT_TAIL(&ch->waiting, wqe, link);
+		if (waited) {
+			TAILQ_INSERT_HEAD(&ch->waiting, wqe, link);	/* it keeps its place */
+		} else {
+			TAILQ_INSERT_TAIL(&ch->waiting, wqe, link);
+		}
 		return;
 	}
 
@@ -809,7 +834,11 @@ rg_submit_rw_request(struct raid_bdev_io *raid_io)
 
 		wqe->cb_fn = _rg_resubmit;
 		wqe->cb_arg = raid_io;
-		TAILQ_INSERT_TAIL(&ch->waiting, wqe, link);
+		if (waited) {
+			TAILQ_INSERT_HEAD(&ch->waiting, wqe, link);
+		} else {
+			TAILQ_INSERT_TAIL(&ch->waiting, wqe, link);
+		}
 		return;
 	}
 	TAILQ_REMOVE(&ch->free_reqs, req, link);
@@ -1108,7 +1137,13 @@ rg_start(struct raid_bdev *raid_bdev)
 	info->refs = 1;
 	/* requests a channel works on at once (raid5_simple.c:14 keeps 128); more of
 	 * them make larger launches when the queue is deep, at n strip buffers each */
-	info->nrequests = RG_REQUESTS_DEFAULT;
+	{
+		const uint64_t stripe_bytes = (uint64_t)raid_bdev->num_base_bdevs * raid_bdev->strip_size *
+					      raid_bdev->bdev.blocklen;
+		const uint64_t fit = stripe_bytes ? RG_POOL_BYTES / stripe_bytes : RG_REQUESTS_DEFAULT;
+
+		info->nrequests = (int)spdk_min(RG_REQUESTS_DEFAULT, spdk_max(RG_REQUESTS_MIN, fit));
+	}
 	if (env_req && atoi(env_req) > 0) {
 		info->nrequests = spdk_min(spdk_max(atoi(env_req), 2), RG_REQUESTS_MAX);
 	}

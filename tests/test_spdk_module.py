@@ -95,6 +95,27 @@ def test_raid6_module_routes_stripes_over_several_device_slots():
 
 
 @pytest.mark.gpu
+def test_raid6_module_with_a_request_pool_of_four():
+    """DRAID_RAID_REQUESTS=4: parent I/O beyond the channel's four stripe requests waits on
+    the channel's retry list and is resubmitted, in submission order, as requests complete
+    (raid5_simple.c:364-370); the same array checks must pass.  (One channel: with several,
+    I/O that waits takes its place in a stripe's queue only when it gets a request, so
+    requests of different channels to one stripe may then run out of submission order --
+    as in the reference, which completes such I/O with NOMEM for the bdev layer to retry,
+    raid5.c:993-997.)"""
+    out = run("spdk_raid_module_test", env={"DRAID_RAID_REQUESTS": "4"})
+    assert "ok raid6 n=10 strip=64KiB" in out and "array checks passed" in out
+    # 32 requests outstanding over a pool of eight: 24 always wait, all complete, none fails
+    import json
+    p = subprocess.run([os.path.join(OUT, "spdk_raid_module_bench"), "6", "10", "64", "32", "0.3"],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, DRAID_RAID_REQUESTS="8"))
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    rows = [json.loads(line) for line in p.stdout.splitlines() if line.startswith("{")]
+    assert len(rows) == 5 and all(r["failed"] == 0 and r["ios"] > 100 for r in rows)
+
+
+@pytest.mark.gpu
 def test_module_on_four_spdk_threads_and_through_hot_remove():
     """raid5.c:496-505,1047-1054: requests of one stripe run one at a time, in arrival
     order, and a finished request hands the stripe to the next one's thread.  Four channels
