@@ -33,9 +33,11 @@ constexpr int kSlots = 16;
 // Pieces a context may hold uploaded but not yet launched (below): the other
 // slots stay free for the pieces a flush packs itself.
 constexpr int kMaxStaged = 12;
-// A launch of at most this many segments reads its descriptors where the host
-// wrote them, in pinned memory, instead of waiting for their upload (stage_piece).
-constexpr size_t kInplaceSegments = 256;
+// A small launch reads its descriptors where the host wrote them, in pinned memory,
+// instead of waiting for their upload (stage_piece).  Small: work items (1 KiB chunks
+// of a stripe) + 16 x segments within this limit -- about 400 stripes of 64 KiB
+// strips, 100 of them cut into 4 KiB runs, 120 of 256 KiB strips.
+constexpr size_t kInplaceLimit = 32768;
 constexpr size_t kPieceBytes = 1u << 20;       // descriptors per launch (≈ 1 MiB)
 constexpr size_t kMinPieceSegments = 4096;
 constexpr uint64_t kMaxSegment = 1ull << 30;
@@ -179,7 +181,7 @@ struct draid_ec_ctx {
     int next = 0;
     int staged_slots = 0;    // slots holding uploaded pieces that wait for their launch
     bool stage_ahead = true; // DRAID_EC_CTX_STAGE_AHEAD=0 turns the early uploads off (A/B, tests)
-    size_t inplace_segments = kInplaceSegments;  // DRAID_EC_CTX_INPLACE_SEGMENTS (A/B, tests)
+    size_t inplace_limit = kInplaceLimit;  // DRAID_EC_CTX_INPLACE_LIMIT (A/B, tests; 0: never)
     uint64_t queued_segments = 0;
     int address_order = 1;  // DRAID_EC_CTX_ADDRESS_ORDER: 0 off, 1 auto, 2 any out-of-order group
                             // (diagnostics and tests)
@@ -656,9 +658,13 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     // start, while the kernel's reads of pinned memory add a PCIe round trip per item,
     // which a launch this small does not notice.  Large launches do (4096 stripes of
     // 4 KiB runs: 1.39 vs 1.00 ms), so they upload.  Wall time of one flush of B
-    // 8+2 stripes at 64 KiB runs, in place vs uploaded: B = 2..32 21-25 vs 41-46 us,
-    // 64: 31 vs 46, 128: 42 vs 53, 256: 59-65 vs 74-75, 1024: encode 198 vs 177.
-    const bool inplace = !ahead && nseg <= c->inplace_segments;
+    // 8+2 stripes at 64 KiB runs (64 items each), in place vs uploaded: B = 2..32
+    // 21-25 vs 41-46 us, 64: 31 vs 46, 128: 42 vs 53, 256: 59-65 vs 74-75, 1024: encode
+    // 198 vs 177; at 4 KiB runs (4 items each) 64 stripes = 1024 segments 65 vs 72,
+    // 256 stripes = 4096 segments 195 vs 176.  That fits about 8 ns per segment (its
+    // row's first trip over the link) plus 0.5 ns per item (the row again, from the
+    // cache) against the upload's 20 us, which is the limit above with some margin.
+    const bool inplace = !ahead && nwork64 + 16 * static_cast<uint64_t>(nseg) <= c->inplace_limit;
     if (inplace && !perm)
         memcpy(h + o_ptr, g.ptrs.data() + s0 * w, nseg * w * sizeof(void*));
     if (perm) {
@@ -921,8 +927,8 @@ int draid_ec_ctx_create(draid_ec_ctx** out)
     // (a context told to sort every group cannot upload pieces in queue order)
     if ((ahead && ahead[0] == '0') || c->address_order == 2)
         c->stage_ahead = false;
-    if (const char* inplace = getenv("DRAID_EC_CTX_INPLACE_SEGMENTS"))
-        c->inplace_segments = strtoul(inplace, nullptr, 0);
+    if (const char* inplace = getenv("DRAID_EC_CTX_INPLACE_LIMIT"))
+        c->inplace_limit = strtoul(inplace, nullptr, 0);
     hipError_t e = hipGetDevice(&c->device);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

@@ -235,12 +235,13 @@ int draid_ec_ctx_update_sg(draid_ec_ctx *ctx, uint32_t k, uint32_t m, uint32_t n
 /* Launch everything queued.  Non-blocking, except that each ~1 MiB piece of
  * descriptors takes one of 16 ring slots and waits for that slot's previous
  * kernel when all 16 are in flight (and allocates the slot's buffers on first
- * use or growth).  A launch of at most 256 segments uploads nothing: its kernel
- * reads the descriptors from the slot's pinned host memory, which takes 20 us off
- * the flush and as much off the time to completion (larger launches upload; the
- * limit can be set with DRAID_EC_CTX_INPLACE_SEGMENTS, 0 = always upload).  The context's stream is non-blocking: it does not wait for
- * work on other streams, so every queued buffer must hold its data when flush
- * is called.
+ * use or growth).  A small launch (about 400 stripes of 64 KiB strips, 100 cut
+ * into 4 KiB runs, 120 of 256 KiB strips) uploads nothing: its kernel reads the
+ * descriptors from the slot's pinned host memory, which takes 20 us off the
+ * flush and as much off the time to completion (larger launches upload; the
+ * limit can be set with DRAID_EC_CTX_INPLACE_LIMIT, 0 = always upload).  The
+ * context's stream is non-blocking: it does not wait for work on other
+ * streams, so every queued buffer must hold its data when flush is called.
  * Order: segments queued with the same (op, k, m) form a group and carry no
  * order among themselves (the flush may run them in address order).  Groups
  * run one after the other on one stream, in the order in which their FIRST

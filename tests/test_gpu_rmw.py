@@ -27,7 +27,7 @@ def _runs(rng, base, length, pieces):
 @pytest.mark.parametrize("uploaded", [False, True])
 def test_rmw_update_matches_reencode(ec, k, m, L, B, uploaded, monkeypatch):
     if uploaded:  # descriptors uploaded first instead of read in place (small launches)
-        monkeypatch.setenv("DRAID_EC_CTX_INPLACE_SEGMENTS", "0")
+        monkeypatch.setenv("DRAID_EC_CTX_INPLACE_LIMIT", "0")
     rng = np.random.default_rng(k * 100 + L)
     n = k + m
     host = np.zeros((B, n, L), np.uint8)

@@ -85,7 +85,7 @@ def test_sg_encode_and_reconstruct(ec, k, m, L, B, prefix, shuffled, uploaded, m
     if shuffled:
         monkeypatch.setenv("DRAID_EC_CTX_ADDRESS_ORDER", "2")  # read at ctx creation
     if uploaded:
-        monkeypatch.setenv("DRAID_EC_CTX_INPLACE_SEGMENTS", "0")
+        monkeypatch.setenv("DRAID_EC_CTX_INPLACE_LIMIT", "0")
     rng = np.random.default_rng(k * L + B)
     pool = Pool(rng, k, m, L, B, prefix=prefix)
     _fill(pool, rng)

@@ -1,6 +1,6 @@
 # The raid module over null base bdevs with its launches' descriptors read in place
 # from pinned memory (the default for launches of up to 256 segments) against uploaded
-# first (DRAID_EC_CTX_INPLACE_SEGMENTS=0), interleaved, plain build for the rates and
+# first (DRAID_EC_CTX_INPLACE_LIMIT=0), interleaved, plain build for the rates and
 # profiling build for the reactor's time per request.  Build first: make -C tests/spdk.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -14,7 +14,7 @@ for round in 1 2; do
     for qd in 32 128; do
       for mode in null ram; do
         for n in 256 0; do
-          DRAID_EC_CTX_INPLACE_SEGMENTS=$n timeout -k 10 120 $B/spdk_raid_module_bench $shape $qd $SEC $mode \
+          DRAID_EC_CTX_INPLACE_LIMIT=$n timeout -k 10 120 $B/spdk_raid_module_bench $shape $qd $SEC $mode \
               | sed "s/^{/{\"build\": \"plain\", \"inplace\": $n, \"round\": $round, /" >> $O || exit 1
         done
       done
@@ -22,7 +22,7 @@ for round in 1 2; do
   done
 done
 for n in 256 0; do
-  DRAID_EC_CTX_INPLACE_SEGMENTS=$n timeout -k 10 120 $B/spdk_raid_module_bench_prof 6 10 64 32 $SEC null \
+  DRAID_EC_CTX_INPLACE_LIMIT=$n timeout -k 10 120 $B/spdk_raid_module_bench_prof 6 10 64 32 $SEC null \
       | sed "s/^{/{\"build\": \"prof\", \"inplace\": $n, \"round\": 1, /" >> $O || exit 1
 done
 python3 - <<'PY'

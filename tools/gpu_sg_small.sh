@@ -8,9 +8,9 @@ mkdir -p gpurun_out
 out=gpurun_out/sg_small_ab.jsonl
 rm -f $out
 for round in 1 2 3; do
-  for b in 2 8 16 32 64 128 256 1024; do
-    for n in ${INPLACE_LIST:-4096 0}; do
-      DRAID_EC_CTX_INPLACE_SEGMENTS=$n timeout -k 10 120 tools/c/sg_bench 65536 $b 300 0 0 | sed "s/^{/{\"inplace\": $n, \"round\": $round, /" >> $out || exit 1
+  for b in ${STRIPES_LIST:-2 8 16 32 64 128 256 1024}; do
+    for n in ${INPLACE_LIST:-1000000 0}; do
+      DRAID_EC_CTX_INPLACE_LIMIT=$n timeout -k 10 120 tools/c/sg_bench ${IOV:-65536} $b 300 0 0 | sed "s/^{/{\"inplace\": $n, \"round\": $round, /" >> $out || exit 1
     done
   done
 done
