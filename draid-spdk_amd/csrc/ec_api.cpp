@@ -49,15 +49,19 @@ namespace {
 
 hipStream_t sync_stream() { return hipStreamPerThread; }
 
-// Per-thread, per-GPU device scratch: a pointer table for calls with more
+// Per-thread, per-GPU scratch: a device pointer table for calls with more
 // vectors than fit in kernel arguments, a 4-byte flag for the *_check calls, and
-// a staging arena for vectors in pageable host memory.  Each is memory of the
-// GPU that was current when it was allocated, so a thread that moves to another
-// GPU (draid_ec_set_device) gets that GPU's own set.
+// a device staging arena for vectors in pageable host memory.  Table and arena
+// are memory of the GPU that was current when they were allocated, so a thread
+// that moves to another GPU (draid_ec_set_device) gets that GPU's own set.
+// The flag is pinned HOST memory (flag_dev: its address on this GPU): the host
+// clears it with a store and reads the verdict with a load, the kernel touches it
+// only when it finds a mismatch -- no memset and no copy back per call.
 struct Scratch {
     void* table = nullptr;
     size_t table_bytes = 0;
     uint32_t* flag = nullptr;
+    uint32_t* flag_dev = nullptr;
     uint8_t* arena = nullptr;
     size_t arena_bytes = 0;
     ~Scratch()
@@ -65,7 +69,7 @@ struct Scratch {
         if (table)
             (void)hipFree(table);
         if (flag)
-            (void)hipFree(flag);
+            (void)hipHostFree(flag);
         if (arena)
             (void)hipFree(arena);
     }
@@ -269,9 +273,15 @@ int check_one(uint32_t k, uint32_t m, int len, void** array)
     if (!sc)
         return -1;
     if (!sc->flag) {
-        hipError_t e = hipMalloc(&sc->flag, sizeof(uint32_t));
-        if (e != hipSuccess)
-            return fail_hip(e, "hipMalloc(flag)");
+        hipError_t e = hipHostMalloc(&sc->flag, 64, hipHostMallocDefault);
+        if (e == hipSuccess)
+            e = hipHostGetDevicePointer(reinterpret_cast<void**>(&sc->flag_dev), sc->flag, 0);
+        if (e != hipSuccess) {
+            if (sc->flag)
+                (void)hipHostFree(sc->flag);
+            sc->flag = nullptr;
+            return fail_hip(e, "hipHostMalloc(flag)");
+        }
     }
     int rc = resolve_stripe(array, static_cast<int>(k + m), 0, static_cast<size_t>(len));
     if (rc)
@@ -281,20 +291,14 @@ int check_one(uint32_t k, uint32_t m, int len, void** array)
     rc = stage_pointers(t_vec.dev.data(), static_cast<int>(k + m), &args, &table);
     if (rc)
         return rc;
-    hipError_t e = hipMemsetAsync(sc->flag, 0, sizeof(uint32_t), sync_stream());
-    if (e != hipSuccess)
-        return fail_hip(e, "hipMemsetAsync(flag)");
-    e = draid::launch_check(k, m, static_cast<uint64_t>(len), table, table ? nullptr : &args,
-                            sc->flag, sync_stream());
-    if (e != hipSuccess)
-        return fail_hip(e, "launch_check");
-    uint32_t host_flag = 0;
-    e = hipMemcpyAsync(&host_flag, sc->flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                       sync_stream());
-    rc = finish_sync(e, "hipMemcpyAsync(flag)");
+    // (the previous call on this thread has been waited for: nothing else writes the flag)
+    __atomic_store_n(sc->flag, 0u, __ATOMIC_RELEASE);
+    rc = finish_sync(draid::launch_check(k, m, static_cast<uint64_t>(len), table,
+                                         table ? nullptr : &args, sc->flag_dev, sync_stream()),
+                     "launch_check");
     if (rc)
         return rc;
-    return host_flag ? 1 : 0;
+    return __atomic_load_n(sc->flag, __ATOMIC_ACQUIRE) ? 1 : 0;
 }
 
 }  // namespace

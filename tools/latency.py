@@ -30,7 +30,13 @@ for k, L in [(4, 65536), (8, 65536), (8, 4096), (16, 262144)]:
         t0 = time.perf_counter()
         ec.xor_gen(ptrs[:k + 1], L)
         xs.append(time.perf_counter() - t0)
+    cs = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        assert ec.pq_check(ptrs, L) == 0
+        cs.append(time.perf_counter() - t0)
     r = {"k": k, "len": L, "pq_gen_us_p50": round(np.median(ts) * 1e6, 1),
+         "pq_check_us_p50": round(np.median(cs) * 1e6, 1),
          "pq_gen_us_p99": round(np.percentile(ts, 99) * 1e6, 1),
          "xor_gen_us_p50": round(np.median(xs) * 1e6, 1)}
     res.append(r)
