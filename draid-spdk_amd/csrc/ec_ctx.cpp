@@ -102,6 +102,9 @@ struct Staged {
     bool uniform = false;           // every segment the same length: no work list
     bool inplace = false;           // the kernel reads the descriptors from the slot's pinned
                                     // host memory: nothing was uploaded
+    bool host_data = false;         // a small launch most of whose segments have strips in host
+                                    // memory: PCIe bound, better with few items resident
+                                    // (LaunchThrottle)
     uint32_t nwork = 0, ulen = 0;   // work items; the uniform length
     size_t o_len = 0, o_fail = 0, o_work = 0;  // offsets into the slot
 };
@@ -129,6 +132,8 @@ struct Group {
     PinnedPtrs ptrs;                // [nseg][w]; op 1: the slot behind the strips holds the
                                     // failure pair in its first two bytes (uploaded with the row)
     std::vector<uint32_t> len;      // [nseg]
+    std::vector<uint8_t> host;      // [nseg] 1: a strip of the segment is pinned / registered HOST
+                                    // memory (known only to a context that resolves host pointers)
     std::vector<uint8_t> fail;      // op 2: [nseg][k/2] exponents
     // Double-buffered pointer storage: a flush whose pieces DMA straight from
     // `ptrs` records uploaded[0] behind those copies and swaps in `spare`, so the
@@ -305,16 +310,18 @@ struct IovIter {
     intptr_t delta;    // device address = p + delta (0 unless the ctx resolves host pointers)
     bool xl;           // resolve each iovec (draid_ec_ctx_set_host_pointers)
     bool bad;          // an iovec was not GPU accessible
+    bool host;         // the iovec the iterator stands in is pinned / registered host memory
     int device;        // the context's GPU: where the kernels will run
 
     // Device-address offset of one iovec, or false when the GPU cannot reach it.
-    static bool resolve(const struct iovec& e, intptr_t* d, int device)
+    static bool resolve(const struct iovec& e, intptr_t* d, int device, bool* host_memory)
     {
         *d = 0;
+        *host_memory = false;
         if (e.iov_len == 0)
             return true;
         const void* dev = nullptr;
-        if (draid::translate(e.iov_base, e.iov_len, &dev, device))
+        if (draid::translate(e.iov_base, e.iov_len, &dev, device, host_memory))
             return false;
         *d = static_cast<const uint8_t*>(dev) - static_cast<const uint8_t*>(e.iov_base);
         return true;
@@ -325,8 +332,12 @@ struct IovIter {
         idx = i;
         p = static_cast<const uint8_t*>(v[i].iov_base);
         left = v[i].iov_len;
-        if (xl && !resolve(v[i], &delta, device))
-            bad = true;
+        if (xl) {
+            bool h = false;
+            if (!resolve(v[i], &delta, device, &h))
+                bad = true;
+            host = h;  // of the iovec the iterator stands in
+        }
     }
 };
 
@@ -363,7 +374,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
     for (uint32_t j = 0; j < n; ++j) {
         if (!iovs || !iovs[j] || !iovcnt || iovcnt[j] < 0)
             return ctx_arg("iovec list missing");
-        it[j] = IovIter{iovs[j], iovcnt[j], 0, nullptr, 0, 0, c->host_pointers, false, c->device};
+        it[j] = IovIter{iovs[j], iovcnt[j], 0, nullptr, 0, 0, c->host_pointers, false, false,
+                        c->device};
         if (len && !iter_seek(it[j], offset ? offset[j] : 0))
             return ctx_arg("iovec list shorter than offset");
         if (it[j].bad)
@@ -400,6 +412,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             if (t.g) {
                 t.g->ptrs.shrink(t.n_ptrs);
                 t.g->len.resize(t.n_len);
+                t.g->host.resize(t.n_len);
                 t.g->fail.resize(t.n_fail);
                 t.g->tail_bytes = t.tail_bytes;
             }
@@ -439,7 +452,8 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                     break;
                 if (t.xl) {  // adjacent for the host: also adjacent for the device?
                     intptr_t d;
-                    if (!IovIter::resolve(t.v[x], &d, t.device) || d != t.delta)
+                    bool h;
+                    if (!IovIter::resolve(t.v[x], &d, t.device, &h) || d != t.delta)
                         break;
                 }
                 avail += t.v[x].iov_len;
@@ -464,11 +478,12 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             return rollback("out of pinned host memory for descriptors");
         const uint8_t* const p0 = it[0].p + it[0].delta;
         int32_t* const off = reinterpret_cast<int32_t*>(out + 1);
-        bool fits = true, bad = false;
+        bool fits = true, bad = false, seg_host = false;
         for (uint32_t j = 0; j < n; ++j) {
             IovIter& t = it[j];
             const uint8_t* const pj = t.p + t.delta;
             ptr[j] = pj;
+            seg_host |= t.host;
             if (may_compact) {
                 const intptr_t d = pj - p0;
                 off[j] = static_cast<int32_t>(d);
@@ -520,6 +535,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
             g.first_seq = c->seq;
         ++c->seq;
         g.len.push_back(static_cast<uint32_t>(run));
+        g.host.push_back(seg_host ? 1 : 0);
         g.tail_bytes += run;
         if (op != 1 && nmeta)
             g.fail.insert(g.fail.end(), meta, meta + nmeta);
@@ -702,6 +718,10 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
         return ctx_fail(e, "hipMemcpyAsync(descriptors)");
     if (!inplace && (e = hipEventRecord(sl.uploaded, c->copy)) != hipSuccess)
         return ctx_fail(e, "descriptor upload event");
+    size_t host_segs = 0;
+    for (size_t i = 0; i < nseg; ++i)
+        host_segs += g.host[perm ? perm[s0 + i] : s0 + i];
+    out->host_data = 2 * host_segs > nseg && nwork64 <= draid::kThrottleItems;
     out->inplace = inplace;
     out->slot = si;
     out->s0 = s0;
@@ -725,6 +745,8 @@ int launch_piece(draid_ec_ctx* c, Group& g, const Staged& st)
     if (!st.inplace && (e = hipStreamWaitEvent(c->stream, sl.uploaded, 0)) != hipSuccess)
         return ctx_fail(e, "descriptor upload event");
     const uint8_t* d = static_cast<const uint8_t*>(st.inplace ? sl.host_dev : sl.dev);
+    // strips in host memory: a PCIe-bound launch runs faster with few items resident
+    draid::LaunchThrottle throttle(st.host_data);
     const auto* tab = reinterpret_cast<const uint8_t* const*>(d);
     const auto* lens = reinterpret_cast<const uint32_t*>(d + st.o_len);
     const void* wl = st.uniform ? nullptr : d + st.o_work;
@@ -814,6 +836,7 @@ int flush_single(draid_ec_ctx* c, Group& g)
     }
     g.ptrs.clear();
     g.len.clear();
+    g.host.clear();
     g.fail.clear();
     g.tail_bytes = 0;
     return e == hipSuccess ? 0 : ctx_fail(e, "launch (single segment)");
@@ -871,12 +894,14 @@ int flush_group(draid_ec_ctx* c, Group& g)
             memmove(rows + i * g.w, rows + static_cast<size_t>(rest[i]) * g.w,
                     g.w * sizeof(void*));
             g.len[i] = g.len[rest[i]];
+            g.host[i] = g.host[rest[i]];
             tail += g.len[i];
             if (nmeta)
                 memmove(g.fail.data() + i * nmeta, g.fail.data() + rest[i] * nmeta, nmeta);
         }
         g.ptrs.shrink(rest.size() * g.w);
         g.len.resize(rest.size());
+        g.host.resize(rest.size());
         g.fail.resize(rest.size() * nmeta);
         g.tail_bytes = tail;
         return rc;
@@ -901,6 +926,7 @@ int flush_group(draid_ec_ctx* c, Group& g)
     }
     g.ptrs.clear();
     g.len.clear();
+    g.host.clear();
     g.fail.clear();
     g.tail_bytes = 0;
     return rc;
@@ -1172,6 +1198,7 @@ int draid_ec_ctx_discard_queued(draid_ec_ctx* c)
         return ctx_arg("ctx is NULL");
     for (Group& g : c->groups) {
         g.len.clear();
+        g.host.clear();
         drop_staged(c, g, 0);
         // the storage may still feed an earlier flush's copies, or this batch's early ones
         if (g.ready() || g.direct)
@@ -1226,6 +1253,7 @@ int draid_ec_ctx_rollback(draid_ec_ctx* c)
         const size_t nmeta = g.fail.size() / have;
         g.ptrs.shrink(keep * g.w);
         g.len.resize(keep);
+        g.host.resize(keep);
         g.fail.resize(keep * nmeta);
         drop_staged(c, g, keep);  // a piece uploaded early that held any of them
     }

@@ -168,6 +168,11 @@ uint8_t* mapped_range(const void* p, uint64_t span)
     return d1 == d0 + (span - 1) ? d0 : nullptr;
 }
 
+uint64_t host_items(const draid_ec_host_stripes* h)
+{
+    return (h->strip_len + draid::kItemBytes - 1) / draid::kItemBytes * h->nstripes;
+}
+
 uint64_t host_span(const draid_ec_host_stripes* h)
 {
     return static_cast<uint64_t>(h->nstripes - 1) * h->stripe_stride +
@@ -176,14 +181,19 @@ uint64_t host_span(const draid_ec_host_stripes* h)
 
 // In-place path over mapped host stripes: one launch, then wait.
 template <class Launch>
-int run_mapped(Launch&& launch)
+int run_mapped(uint64_t items, Launch&& launch)
 {
     HostEngine& eng = engine();
     Stage& s = eng.st[0];
     hipError_t e;
     if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
         return draid::fail_hip(e, "hipStreamCreate(host engine)");
-    if ((e = launch(eng, s.stream)) != hipSuccess)
+    {
+        // every strip crosses PCIe: a small launch runs faster with few items resident
+        draid::LaunchThrottle throttle(items <= draid::kThrottleItems);
+        e = launch(eng, s.stream);
+    }
+    if (e != hipSuccess)
         return draid::fail_hip(e, "launch (mapped host stripes)");
     if ((e = hipStreamSynchronize(s.stream)) != hipSuccess)
         return draid::fail_hip(e, "hipStreamSynchronize(mapped host stripes)");
@@ -243,7 +253,7 @@ int draid_ec_host_encode(const draid_ec_host_stripes* h, uint32_t chunk_stripes)
     const uint64_t S = h->strip_len;
     if (!(h->flags & DRAID_EC_HOST_STAGED))
         if (uint8_t* d = mapped_range(h->base, host_span(h)))
-            return run_mapped([&](HostEngine&, hipStream_t st) {
+            return run_mapped(host_items(h), [&](HostEngine&, hipStream_t st) {
                 return draid::launch_encode_strided(k, m, S, h->nstripes, d, h->strip_stride,
                                                     h->stripe_stride, st);
             });
@@ -293,7 +303,7 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
     }
     if (!(h->flags & DRAID_EC_HOST_STAGED))
         if (uint8_t* d = mapped_range(h->base, host_span(h)))
-            return run_mapped([&](HostEngine& eng, hipStream_t st) {
+            return run_mapped(host_items(h), [&](HostEngine& eng, hipStream_t st) {
                 const size_t fb = 2 * static_cast<size_t>(h->nstripes);
                 hipError_t e;
                 if (eng.zfail_bytes < fb) {

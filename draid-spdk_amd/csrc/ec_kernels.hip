@@ -34,6 +34,7 @@
 // the hot path).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -56,6 +57,50 @@ namespace draid {
 static int g_variant = 0;
 void set_variant(int v) { g_variant = DRAID_EC_LAB ? v : 0; }
 int get_variant() { return g_variant; }
+
+// Dynamic LDS added to every launch of the calling thread while a LaunchThrottle is
+// alive.  No kernel uses it: LDS a workgroup holds is LDS its CU cannot give to
+// another, so it bounds how many items are resident per CU without a second
+// instance of any kernel.  Launches whose strips live in HOST memory want that:
+// every resident item has all its reads queued on the PCIe link at once, and a
+// launch of a few dozen stripes pays for the last generation of items draining
+// together -- the fewer are resident, the less.
+thread_local uint32_t t_launch_lds = 0;
+static inline uint32_t launch_lds() { return t_launch_lds; }
+// One item per CU (8+2 x 64 KiB stripes in pinned memory, us per launch of B stripes, no
+// extra LDS / 56 KiB (two items per CU) / 128 KiB (one): B = 16 203 / 184 / 170, 32: 372 /
+// 344 / 321, 64: 675 / 657 / 634, 256: 2478 / 2482 / 2423, 1024 the same; the dual
+// reconstruct alike.  The same LDS on stripes in HBM costs a factor of four, and launches
+// much larger than the CUs hold at once lose a few per cent to it: kThrottleItems.)
+constexpr int kThrottleLds = 128 * 1024;
+static uint32_t throttle_bytes()
+{
+    // once per thread and device would be exact; one query serves: every GPU of a node is
+    // the same part.  DRAID_EC_THROTTLE_LDS (bytes, 0 = off) overrides, for A/B runs.
+    static const uint32_t bytes = [] {
+        if (const char* e = getenv("DRAID_EC_THROTTLE_LDS"))
+            return static_cast<uint32_t>(strtoul(e, nullptr, 0));
+        int dev = 0, max_block = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&max_block, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) !=
+                hipSuccess)
+            return 0u;
+        // room left for the largest static allocation of any kernel here (the column
+        // reconstruct's k + 2 rows of 1 KiB at k = 20)
+        const int room = max_block - 24 * 1024;
+        return static_cast<uint32_t>(room > kThrottleLds ? kThrottleLds : room > 0 ? room : 0);
+    }();
+    return bytes;
+}
+LaunchThrottle::LaunchThrottle(bool on) : prev_(t_launch_lds)
+{
+    if (on)
+        t_launch_lds = throttle_bytes();
+}
+LaunchThrottle::~LaunchThrottle() { t_launch_lds = prev_; }
+// Test / measurement hook (not in the public header): dynamic LDS on every later
+// launch of the calling thread.
+extern "C" void draid_ec_test_launch_lds(uint32_t bytes) { t_launch_lds = bytes; }
 
 // ------------------------------------------------------------ launchers
 
@@ -151,14 +196,14 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
     if constexpr (C::SPLIT > 1) {
         ItemGrid ig;
         const dim3 g = split_grid(cps, nstripes, ig);
-        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
+        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
                            static_cast<uint32_t>(len), cps, nstripes, flag, ig);
     } else if constexpr (KT > 0 && std::is_same<Ptrs, TablePtrs>::value)
-        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), 0,
+        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), launch_lds(),
                            st, TablePlain{pp.tab, pp.stride}, k, static_cast<uint32_t>(len), cps,
                            nstripes, flag);
     else
-        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp,
+        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
                            k, static_cast<uint32_t>(len), cps, nstripes, flag);
     return hipGetLastError();
 }
@@ -178,13 +223,13 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
         ItemGrid ig;
         const dim3 g = split_grid(cps, nstripes, ig);
         if constexpr (BYSTRIP)
-            hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
+            hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
                                static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
         else
-            hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), 0, st, pp,
+            hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
                                static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
     } else {
-        hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), 0, st, pp,
+        hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
                            k, static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
     }
     return hipGetLastError();
@@ -624,18 +669,18 @@ static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, uint32_t
     if constexpr (C::SPLIT > 1) {
         if (row_bytes)
             hipLaunchKernelGGL((k_encode_work_split<KT, M, C, RowOffs>), dim3(nwork),
-                               dim3(C::NTHR), 0, st, rows, work_src<C>(seg_len, work, ulen),
+                               dim3(C::NTHR), launch_lds(), st, rows, work_src<C>(seg_len, work, ulen),
                                nwork);
         else
-            hipLaunchKernelGGL((k_encode_work_split<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+            hipLaunchKernelGGL((k_encode_work_split<KT, M, C>), dim3(nwork), dim3(C::NTHR), launch_lds(), st,
                                TablePtrs{tab, k + M}, work_src<C>(seg_len, work, ulen), nwork);
     } else {
         if (row_bytes)
             hipLaunchKernelGGL((k_encode_work<KT, M, false, C, RowOffs>), dim3(nwork),
-                               dim3(C::NTHR), 0, st, rows, k, work_src<C>(seg_len, work, ulen),
+                               dim3(C::NTHR), launch_lds(), st, rows, k, work_src<C>(seg_len, work, ulen),
                                nwork);
         else
-            hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), 0,
+            hipLaunchKernelGGL((k_encode_work<KT, M, false, C>), dim3(nwork), dim3(C::NTHR), launch_lds(),
                                st, WorkEncPtrs<KT>{tab, k + M}, k,
                                work_src<C>(seg_len, work, ulen), nwork);
     }
@@ -654,19 +699,19 @@ static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t tstrid
     if constexpr (C::SPLIT > 1) {
         if (row_bytes)
             hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C, RowOffs>), dim3(nwork),
-                               dim3(C::NTHR), 0, st, rows, work_src<C>(seg_len, work, ulen), fail,
+                               dim3(C::NTHR), launch_lds(), st, rows, work_src<C>(seg_len, work, ulen), fail,
                                fstride, nwork);
         else
-            hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0,
+            hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C>), dim3(nwork), dim3(C::NTHR), launch_lds(),
                                st, TablePtrs{tab, tstride}, work_src<C>(seg_len, work, ulen), fail,
                                fstride, nwork);
     } else {
         if (row_bytes)
             hipLaunchKernelGGL((k_reconstruct_work<KT, M, C, RowOffs>), dim3(nwork), dim3(C::NTHR),
-                               0, st, rows, k, work_src<C>(seg_len, work, ulen), fail, fstride,
+                               launch_lds(), st, rows, k, work_src<C>(seg_len, work, ulen), fail, fstride,
                                nwork);
         else
-            hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), 0, st,
+            hipLaunchKernelGGL((k_reconstruct_work<KT, M, C>), dim3(nwork), dim3(C::NTHR), launch_lds(), st,
                                TablePtrs{tab, tstride}, k, work_src<C>(seg_len, work, ulen), fail,
                                fstride, nwork);
     }
@@ -762,7 +807,7 @@ static hipError_t go_update_work(uint32_t nd, const uint8_t* const* table, const
 {
     using C = EncCfg<1, 0, DRAID_UPD_WAVES>;  // buffer nt loads, write-through nt stores
     const WorkSrc ws = work_src<C>(seg_len, work, ulen);
-    hipLaunchKernelGGL((k_update_work<M, NDT, C>), dim3(nwork), dim3(C::NTHR), 0, st, table, nd,
+    hipLaunchKernelGGL((k_update_work<M, NDT, C>), dim3(nwork), dim3(C::NTHR), launch_lds(), st, table, nd,
                        exps, ws, nwork);
     return hipGetLastError();
 }
@@ -822,7 +867,7 @@ hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t
         tri_words(p[0], p[1], p[2], t.t0);
         tri_words(p[3], p[4], p[5], t.t1);
         t.t2 = (p[6] << 8) | (p[7] << 16) | ((p[6] ^ p[7]) << 24);
-        hipLaunchKernelGGL((k_gf_vect_mul<MulTable, NTHR, U, POL>), grid, dim3(NTHR), 0, st, src,
+        hipLaunchKernelGGL((k_gf_vect_mul<MulTable, NTHR, U, POL>), grid, dim3(NTHR), launch_lds(), st, src,
                            dst, static_cast<uint32_t>(len), t);
     } else {
         NibTable t;
@@ -833,7 +878,7 @@ hipError_t launch_gf_vect_mul(uint64_t len, const uint8_t tbl[32], const uint8_t
                       (tbl[16 + 4 * w + 2] << 16) |
                       (static_cast<uint32_t>(tbl[16 + 4 * w + 3]) << 24);
         }
-        hipLaunchKernelGGL((k_gf_vect_mul<NibTable, NTHR, U, POL>), grid, dim3(NTHR), 0, st, src,
+        hipLaunchKernelGGL((k_gf_vect_mul<NibTable, NTHR, U, POL>), grid, dim3(NTHR), launch_lds(), st, src,
                            dst, static_cast<uint32_t>(len), t);
     }
     return hipGetLastError();

@@ -100,8 +100,31 @@ int fail_arg(const char* what);
 // Results are cached per thread; translate_invalidate() empties every thread's
 // cache.
 constexpr int kCurrentDevice = -2;
-int translate(const void* p, size_t len, const void** dev, int on_device = kCurrentDevice);
+// *host_memory (may be null): the range is pinned / registered HOST memory.
+int translate(const void* p, size_t len, const void** dev, int on_device = kCurrentDevice,
+              bool* host_memory = nullptr);
 void translate_invalidate();
+
+// While one is alive (and `on`), every launch of the calling thread carries dynamic
+// LDS that no kernel uses, which bounds the items resident per CU: for launches
+// whose strips live in host memory (see ec_kernels.hip, t_launch_lds).
+// It pays for launches of up to about this many work items (1 KiB chunks of a stripe) --
+// the raid module over null base bdevs, MiB/s throttled vs not: 8+2 x 64 KiB full-stripe
+// writes at 16 requests per launch (1024 items) 41.4k vs 36.6k, at 32 (2048 items) 44.0k
+// vs 42.7k, at 64 (4096 items) 44.2k vs 46.4k; 16+2 x 256 KiB at 16 per launch (4096
+// items) 46.5k vs 47.4k; a degraded read at 43 requests per launch (2730 items) 54.3k vs
+// 56.9k.
+constexpr uint64_t kThrottleItems = 2048;
+class LaunchThrottle {
+public:
+    explicit LaunchThrottle(bool on);
+    ~LaunchThrottle();
+    LaunchThrottle(const LaunchThrottle&) = delete;
+    LaunchThrottle& operator=(const LaunchThrottle&) = delete;
+
+private:
+    uint32_t prev_;
+};
 
 // Variant selector for A/B experiments inside one process (0 = default).
 void set_variant(int v);

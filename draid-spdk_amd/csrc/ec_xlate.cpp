@@ -38,6 +38,7 @@ struct Range {
     uintptr_t lo = 0, hi = 0;  // host-side name of the range: [lo, hi)
     intptr_t delta = 0;        // device address = host address + delta
     int device = draid::kAnyDevice;  // the GPU whose memory it is; host memory: any
+    bool host = false;               // pinned / registered host memory: every access crosses PCIe
 };
 
 constexpr int kWays = 32;
@@ -71,6 +72,7 @@ int query(const void* p, size_t len, Range* out)
         // the start of its mapping depending on the runtime version
         const uintptr_t hp = a.hostPointer ? reinterpret_cast<uintptr_t>(a.hostPointer) : q;
         dev = reinterpret_cast<uintptr_t>(a.devicePointer) + (q - hp);
+        out->host = true;
     } else {
         return 1;  // pageable host memory, arrays, mappings without a device address
     }
@@ -139,9 +141,11 @@ static bool usable(const Range& r, int on_device)
     return range_usable_on(r.device, on_device == kCurrentDevice ? current_device() : on_device);
 }
 
-int translate(const void* p, size_t len, const void** dev, int on_device)
+int translate(const void* p, size_t len, const void** dev, int on_device, bool* host_memory)
 {
     *dev = nullptr;
+    if (host_memory)
+        *host_memory = false;
     if (!p)
         return 1;
     Cache& c = t_cache;
@@ -161,6 +165,8 @@ int translate(const void* p, size_t len, const void** dev, int on_device)
             if (!usable(hit, on_device))
                 return 2;  // another GPU's memory
             *dev = reinterpret_cast<const void*>(q + static_cast<uintptr_t>(hit.delta));
+            if (host_memory)
+                *host_memory = hit.host;
             return 0;
         }
     }
@@ -175,6 +181,8 @@ int translate(const void* p, size_t len, const void** dev, int on_device)
     if (!usable(r, on_device))
         return 2;
     *dev = reinterpret_cast<const void*>(q + static_cast<uintptr_t>(r.delta));
+    if (host_memory)
+        *host_memory = r.host;
     return 0;
 }
 
