@@ -271,7 +271,9 @@ int draid_ec_ctx_ticket_query(draid_ec_ctx *ctx, uint64_t ticket);
  * pointer -- and is resolved to its device address while the descriptors are
  * written (draid_ec_device_pointer's cached lookup, one per iovec).  A stripe
  * with an iovec the GPU cannot reach is rejected with 1 and queues nothing.
- * Off by default. */
+ * The context then also knows which segments lie in host memory, and launches
+ * small batches of those with fewer workgroups resident per CU (a PCIe-bound
+ * launch of a few dozen stripes is 14-18% faster that way).  Off by default. */
 int draid_ec_ctx_set_host_pointers(draid_ec_ctx *ctx, int on);
 int draid_ec_ctx_query(draid_ec_ctx *ctx);
 int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);
