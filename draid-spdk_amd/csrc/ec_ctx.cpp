@@ -41,6 +41,7 @@ constexpr size_t kInplaceLimit = 32768;
 constexpr size_t kPieceBytes = 1u << 20;       // descriptors per launch (≈ 1 MiB)
 constexpr size_t kMinPieceSegments = 4096;
 constexpr uint64_t kMaxSegment = 1ull << 30;
+constexpr uint64_t kWideFlushes = 64;  // see draid_ec_ctx::wide_until
 
 // Growable array in pinned host memory.  The walk writes a group's strip
 // pointers here and the flush DMAs them to the device straight from it, so the
@@ -195,6 +196,12 @@ struct draid_ec_ctx {
     uint64_t seq = 0;        // segments queued so far (orders the groups of a flush)
     bool host_pointers = false;  // iov_base values are the caller's host addresses: resolve them
     bool compact_rows = true;    // DRAID_EC_CTX_ROWS=64 turns compact rows off (A/B, tests)
+    // A run whose strips lie more than 2 GiB apart goes into a group of its own, which is a
+    // launch of its own: a caller whose buffers are spread like that (a request pool far from
+    // the user buffers) would pay two launches per flush for as long as some runs fit and
+    // some do not.  So after such a run every row is a row of pointers until kWideFlushes
+    // flushes have passed without one.
+    uint64_t flushes = 0, wide_until = 0;
     int fail_after = 0;      // test hook: the n-th piece from now fails before it launches
     // Flush tickets: an event recorded behind each ticketed flush, so a poller can
     // complete the requests of one flush while later ones are still running.
@@ -420,7 +427,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
         c->seq = n_seq;
         return ctx_arg(what);
     };
-    const bool may_compact = c->compact_rows && op != 2;
+    bool may_compact = c->compact_rows && op != 2 && c->flushes >= c->wide_until;
     const uint8_t* ptr[512];
     uintptr_t fpair = 0;
     if (op == 1)
@@ -514,6 +521,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                 off[n] = static_cast<int32_t>(fpair);  // the failure pair rides behind the strips
         } else {
             if (may_compact) {  // strips more than 2 GiB apart: a row of pointers after all
+                c->wide_until = c->flushes + kWideFlushes;
                 gp->ptrs.shrink(gp->ptrs.size() - gp->w);
                 if (!(gp = use(false))) {
                     const int rc = ready_rc;
@@ -526,6 +534,7 @@ int walk(draid_ec_ctx* c, int op, uint32_t k, uint32_t m, const struct iovec* co
                     return rollback("out of pinned host memory for descriptors");
                 for (uint32_t j = 0; j < n; ++j)
                     out[j] = ptr[j];
+                may_compact = false;  // the rest of this stripe's runs too
             }
             if (op == 1)
                 out[n] = reinterpret_cast<const void*>(fpair);
@@ -1103,6 +1112,7 @@ int draid_ec_ctx_flush(draid_ec_ctx* c)
         rc = flush_group(c, *gp[i]);
     recount(c);  // on failure: exactly the segments that did not launch
     c->level = 0;
+    ++c->flushes;
     return rc;
 }
 
