@@ -162,6 +162,10 @@ int main(int argc, char **argv)
     int inflight[MAX_GROUPS];
     for (int g = 0; g < groups; g++)
         OK(draid_ec_ctx_create(&ctx[g]));
+    /* the contexts look the addresses up themselves (a cached range lookup per iovec):
+     * they then know that these launches read host memory and size them for the link */
+    for (int g = 0; g < groups; g++)
+        OK(draid_ec_ctx_set_host_pointers(ctx[g], 1));
 
     /* warm-up: one pass of every group */
     for (int g = 0; g < groups; g++) {
