@@ -50,6 +50,7 @@ struct task {
 	struct job *job;
 	struct iovec iov;
 	uint8_t *buf;
+	uint64_t done;	/* this task's completed I/Os: a task that waits forever shows here */
 };
 
 struct job {
@@ -81,6 +82,9 @@ task_done(struct spdk_bdev_io *bdev_io, bool success, void *cb_arg)
 	spdk_bdev_free_io(bdev_io);
 	j->outstanding--;
 	j->done++;
+	if (!j->draining) {
+		t->done++;
+	}
 	if (!success) {
 		j->failed++;
 	}
@@ -155,6 +159,17 @@ run_job(const char *name, struct raid_bdev *raid, struct spdk_io_channel *ch,
 	       (unsigned long long)(s1.flushes - s0.flushes),
 	       s1.flushes > s0.flushes ? (double)(s1.gpu_requests - s0.gpu_requests) /
 	       (double)(s1.flushes - s0.flushes) : 0.0);
+	{
+		uint64_t lo = UINT64_MAX, hi = 0;
+
+		for (i = 0; i < qd; i++) {
+			lo = spdk_min(lo, tasks[i].done);
+			hi = spdk_max(hi, tasks[i].done);
+		}
+		/* before the drain: how evenly the outstanding I/Os were served */
+		printf(", \"task_ios_min\": %llu, \"task_ios_max\": %llu", (unsigned long long)lo,
+		       (unsigned long long)hi);
+	}
 	printf(", \"reactor_us_per_request\": %.3f", (t1 - t0) * 1e6 / (double)j.done);
 	if (pr.map.calls) {
 		/* module sections, microseconds of reactor time per completed request */

@@ -113,6 +113,10 @@ def test_raid6_module_with_a_request_pool_of_four():
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     rows = [json.loads(line) for line in p.stdout.splitlines() if line.startswith("{")]
     assert len(rows) == 5 and all(r["failed"] == 0 and r["ios"] > 100 for r in rows)
+    # waiting I/O is served in submission order: no task is left behind while the others
+    # resubmit from their completion callbacks
+    for r in rows:
+        assert r["task_ios_min"] * 2 >= r["task_ios_max"] > 0, r
 
 
 @pytest.mark.gpu
