@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/draid_ec.h"
@@ -64,6 +65,14 @@ struct Scratch {
     uint32_t* flag_dev = nullptr;
     uint8_t* arena = nullptr;
     size_t arena_bytes = 0;
+    // Pageable vectors of an ordinary call (a stripe of 64 KiB strips) do not go through the
+    // device arena but through this pinned HOST one: the CPU copies them in, the kernel
+    // reads and writes them there over PCIe, the CPU copies the results out -- two or three
+    // runtime copies of pageable memory per call cost more than the call (bounce_dev: the
+    // arena's address on this GPU).
+    uint8_t* bounce = nullptr;
+    uint8_t* bounce_dev = nullptr;
+    size_t bounce_bytes = 0;
     ~Scratch()
     {
         if (table)
@@ -72,8 +81,13 @@ struct Scratch {
             (void)hipHostFree(flag);
         if (arena)
             (void)hipFree(arena);
+        if (bounce)
+            (void)hipHostFree(bounce);
     }
 };
+// Calls that stage more than this go through the device arena (the copies then run at the
+// runtime's pageable rate either way, and pinned memory is not for hoarding).
+constexpr size_t kBounceMax = 8u << 20;
 thread_local draid::PerDevice<Scratch> t_scratch_of;
 
 // The calling thread's scratch on its current GPU; null (with the error
@@ -115,6 +129,7 @@ struct Vectors {
     std::vector<Staged> staged;
     size_t len = 0;
     uint8_t* arena = nullptr;  // the staging arena the offsets refer to (this call's GPU)
+    uint8_t* bounce = nullptr; // ... or the pinned host arena, as the CPU sees it
 
     int resolve(void* const* host, const uint8_t* use, int n, size_t bytes)
     {
@@ -145,11 +160,41 @@ struct Vectors {
             staged[slot[i]].use |= use[i];
         }
         arena = nullptr;
+        bounce = nullptr;
         if (staged.empty())
             return 0;
         Scratch* sc = scratch();
         if (!sc)
             return -1;
+        if (need <= kBounceMax) {
+            if (sc->bounce_bytes < need) {
+                if (sc->bounce)
+                    (void)hipHostFree(sc->bounce);
+                sc->bounce = sc->bounce_dev = nullptr;
+                sc->bounce_bytes = 0;
+                const size_t cap = std::max<size_t>(need, 1u << 20);
+                hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&sc->bounce), cap,
+                                             hipHostMallocDefault);
+                if (e == hipSuccess)
+                    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&sc->bounce_dev),
+                                                sc->bounce, 0);
+                if (e != hipSuccess) {
+                    if (sc->bounce)
+                        (void)hipHostFree(sc->bounce);
+                    sc->bounce = nullptr;
+                    return fail_hip(e, "hipHostMalloc(staging for pageable vectors)");
+                }
+                sc->bounce_bytes = cap;
+            }
+            bounce = sc->bounce;
+            for (int i = 0; i < n; ++i)
+                if (slot[i] >= 0)
+                    dev[i] = sc->bounce_dev + staged[slot[i]].offset;
+            for (const Staged& s : staged)
+                if (s.use & kIn)
+                    memcpy(bounce + s.offset, s.host, bytes);
+            return 0;
+        }
         if (sc->arena_bytes < need) {
             if (sc->arena)
                 (void)hipFree(sc->arena);
@@ -178,6 +223,8 @@ struct Vectors {
     // Queues the copies back to pageable destinations (before the final wait).
     hipError_t write_back() const
     {
+        if (bounce)
+            return hipSuccess;  // copied out by the CPU after the wait (copy_out)
         for (const Staged& s : staged) {
             if (!(s.use & kOut))
                 continue;
@@ -187,6 +234,16 @@ struct Vectors {
                 return e;
         }
         return hipSuccess;
+    }
+
+    // After the wait: results from the pinned arena to their pageable destinations.
+    void copy_out() const
+    {
+        if (!bounce)
+            return;
+        for (const Staged& s : staged)
+            if (s.use & kOut)
+                memcpy(s.host, bounce + s.offset, len);
     }
 };
 thread_local Vectors t_vec;
@@ -248,6 +305,7 @@ int finish_sync(hipError_t e, const char* what)
     e = hipStreamSynchronize(sync_stream());
     if (e != hipSuccess)
         return fail_hip(e, "hipStreamSynchronize");
+    t_vec.copy_out();
     return 0;
 }
 
