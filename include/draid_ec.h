@@ -12,8 +12,9 @@
  *     user iovecs (raid5.c:188-201) -- any kind of pointer: device memory is
  *     used in place; pinned or registered host memory is read and written in
  *     place through its device address (looked up per call, cached per thread);
- *     pageable host memory is copied through a per-thread device staging
- *     buffer.  No pointer the GPU cannot reach is ever handed to a kernel.
+ *     pageable host memory is copied through a per-thread staging buffer
+ *     (pinned host memory for calls that stage up to 8 MiB, device memory
+ *     beyond).  No pointer the GPU cannot reach is ever handed to a kernel.
  *     Calls are synchronous, like isa-l's: they run on the calling thread's
  *     per-thread stream and return once the result is in memory.
  *
