@@ -34,9 +34,12 @@ def oracle_pq(data: np.ndarray):
     return s[0, k].copy(), s[0, k + 1].copy()
 
 
-@pytest.mark.parametrize("k,L", [(4, 65536), (8, 4096), (14, 4096), (40, 1024 + 32)])
+@pytest.mark.parametrize("k,L", [(4, 65536), (8, 4096), (14, 4096), (40, 1024 + 32),
+                                 (8, 1 << 20), (6, (2 << 20) + 64)])
 def test_pq_gen_on_pageable_host_memory(ec, k, L):
-    """malloc'd (numpy) vectors: staged in, P and Q staged out, sources untouched."""
+    """malloc'd (numpy) vectors: staged in, P and Q staged out, sources untouched.  Calls
+    that stage up to 8 MiB go through a pinned host arena, larger ones (the last two
+    cases: 10 and 16 MiB) through a device arena and the runtime's copies."""
     rng = np.random.default_rng(k * L)
     vec = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
     p = np.full(L, 0xAA, np.uint8)
