@@ -10,6 +10,10 @@
 // protects each staging area: its next chunk's copy-in is queued behind its
 // previous chunk's copy-out.  The calls are synchronous.
 //
+// (That is the path DRAID_EC_HOST_STAGED selects, and the one host memory takes that the
+// runtime knows but that is not one mapping.  Pageable memory does not use the runtime's
+// copies at all: run_bounce below.)
+//
 // When the stripes are pinned or registered host memory (what SPDK's hugepage
 // buffers become after draid_ec_host_register) the staging is skipped: one
 // launch over the strided layout reads the strips it needs in place over PCIe
@@ -42,9 +46,20 @@ struct Stage {
     uint64_t S = 0;
 };
 
+// One of two pinned buffers the pageable path bounces chunks of stripes through.
+struct Bounce {
+    hipStream_t stream = nullptr;
+    uint8_t* host = nullptr;  // pinned: [rows][k+m][S], then the chunk's failure pairs
+    uint8_t* dev = nullptr;   // the same memory as the GPU addresses it
+    size_t bytes = 0;
+    bool busy = false;        // a kernel over it has been launched and not waited for
+    uint32_t c0 = 0, rows = 0;
+};
+
 struct HostEngine {
     int device = -1;
     Stage st[kStreams];
+    Bounce bn[2];
     uint8_t* zfail = nullptr;  // device copy of the fail table (zero-copy path)
     size_t zfail_bytes = 0;
     ~HostEngine() { reset(); }
@@ -54,6 +69,15 @@ struct HostEngine {
             (void)hipFree(zfail);
         zfail = nullptr;
         zfail_bytes = 0;
+        for (Bounce& b : bn) {
+            if (b.stream) {
+                (void)hipStreamSynchronize(b.stream);
+                (void)hipStreamDestroy(b.stream);
+            }
+            if (b.host)
+                (void)hipHostFree(b.host);
+            b = Bounce();
+        }
         for (Stage& s : st) {
             if (s.stream)
                 (void)hipStreamSynchronize(s.stream);
@@ -240,6 +264,115 @@ int run_chunks(const draid_ec_host_stripes* h, uint32_t chunk, uint32_t in_lo, u
     return 0;
 }
 
+// Pageable stripes.  The runtime's copies of pageable memory are slow -- strided ones
+// (hipMemcpy2DAsync, a row per strip) run at 4 GiB/s of user data on the shapes below,
+// where the same calls on pinned memory reach 35-50 -- so this path does not use them:
+// the CPU copies a chunk of stripes into a pinned buffer (only the strips the kernel
+// reads), the kernel works on the buffer in place over PCIe like the mapped path, and
+// the CPU copies the strips it wrote back out.  Two buffers: the GPU works on one chunk
+// while the CPU moves the next one in and the previous one out.  fail == nullptr: encode.
+int run_bounce(const draid_ec_host_stripes* h, const uint8_t* fail)
+{
+    const uint32_t k = h->k, m = h->m, n = k + m;
+    const uint64_t S = h->strip_len;
+    const uint64_t stripe_bytes = n * S;
+    // chunks of about 16 MiB: small enough for the copies of one to hide behind the
+    // kernel of another, small enough to run throttled (LaunchThrottle)
+    const uint32_t chunk = static_cast<uint32_t>(
+        std::min<uint64_t>(h->nstripes, std::max<uint64_t>(1, (16u << 20) / stripe_bytes)));
+    const size_t need = static_cast<size_t>(chunk) * stripe_bytes + 2 * static_cast<size_t>(chunk);
+    HostEngine& eng = engine();
+    hipError_t e;
+    for (Bounce& b : eng.bn) {
+        if (!b.stream &&
+            (e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking)) != hipSuccess)
+            return draid::fail_hip(e, "hipStreamCreate(host engine)");
+        if (b.bytes < need) {
+            if (b.host)
+                (void)hipHostFree(b.host);
+            b.host = b.dev = nullptr;
+            b.bytes = 0;
+            if ((e = hipHostMalloc(reinterpret_cast<void**>(&b.host), need,
+                                   hipHostMallocDefault)) != hipSuccess)
+                return draid::fail_hip(e, "hipHostMalloc(bounce buffer for pageable stripes)");
+            if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&b.dev), b.host, 0)) !=
+                hipSuccess)
+                return draid::fail_hip(e, "hipHostGetDevicePointer(bounce buffer)");
+            b.bytes = need;
+        }
+        b.busy = false;
+    }
+    uint8_t* base = static_cast<uint8_t*>(h->base);
+    // the strips of stripe s the kernel writes: parity (encode) or the lost ones
+    auto written = [&](uint32_t s, uint32_t j) {
+        if (!fail)
+            return j >= k;
+        return fail[2 * static_cast<size_t>(s)] == j || fail[2 * static_cast<size_t>(s) + 1] == j;
+    };
+    auto finish = [&](Bounce& b) -> int {
+        if (!b.busy)
+            return 0;
+        b.busy = false;
+        if ((e = hipStreamSynchronize(b.stream)) != hipSuccess)
+            return draid::fail_hip(e, "hipStreamSynchronize(pageable stripes)");
+        for (uint32_t r = 0; r < b.rows; ++r)
+            for (uint32_t j = 0; j < n; ++j)
+                if (written(b.c0 + r, j))
+                    memcpy(base + static_cast<uint64_t>(b.c0 + r) * h->stripe_stride +
+                               j * h->strip_stride,
+                           b.host + (static_cast<uint64_t>(r) * n + j) * S, S);
+        return 0;
+    };
+    int rc = 0;
+    for (uint32_t c0 = 0, ci = 0; c0 < h->nstripes && rc == 0; c0 += chunk, ++ci) {
+        Bounce& b = eng.bn[ci & 1];
+        if ((rc = finish(b)) != 0)
+            break;
+        b.c0 = c0;
+        b.rows = std::min(chunk, h->nstripes - c0);
+        for (uint32_t r = 0; r < b.rows; ++r) {
+            const size_t s = static_cast<size_t>(c0) + r;
+            if (fail && fail[2 * s] == DRAID_EC_FAIL_NONE && fail[2 * s + 1] == DRAID_EC_FAIL_NONE)
+                continue;  // nothing lost: the kernel skips the stripe, so nothing is read
+            for (uint32_t j = 0; j < n; ++j)
+                if (!written(c0 + r, j))
+                    memcpy(b.host + (static_cast<uint64_t>(r) * n + j) * S,
+                           base + static_cast<uint64_t>(c0 + r) * h->stripe_stride +
+                               j * h->strip_stride,
+                           S);
+        }
+        const uint64_t items = (S + draid::kItemBytes - 1) / draid::kItemBytes * b.rows;
+        draid::LaunchThrottle throttle(items <= draid::kThrottleItems);
+        if (fail) {
+            uint8_t* f = b.host + static_cast<size_t>(chunk) * stripe_bytes;
+            memcpy(f, fail + 2 * static_cast<size_t>(c0), 2 * static_cast<size_t>(b.rows));
+            e = draid::launch_reconstruct_strided(k, m, S, b.rows, b.dev, S, stripe_bytes,
+                                                  b.dev + static_cast<size_t>(chunk) * stripe_bytes,
+                                                  nullptr, b.stream);
+        } else {
+            e = draid::launch_encode_strided(k, m, S, b.rows, b.dev, S, stripe_bytes, b.stream);
+        }
+        if (e != hipSuccess) {
+            rc = draid::fail_hip(e, "launch (pageable stripes)");
+            break;
+        }
+        b.busy = true;
+    }
+    for (Bounce& b : eng.bn) {
+        const int r2 = finish(b);  // also after a failure: nothing may still run on the buffers
+        if (rc == 0)
+            rc = r2;
+    }
+    return rc;
+}
+
+// Pageable memory: the GPU runtime does not know the range at all.
+bool is_pageable(const draid_ec_host_stripes* h)
+{
+    const void* d = nullptr;
+    return draid::translate(h->base, 1, &d) == 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -251,12 +384,15 @@ int draid_ec_host_encode(const draid_ec_host_stripes* h, uint32_t chunk_stripes)
         return rc;
     const uint32_t k = h->k, m = h->m, n = k + m;
     const uint64_t S = h->strip_len;
-    if (!(h->flags & DRAID_EC_HOST_STAGED))
+    if (!(h->flags & DRAID_EC_HOST_STAGED)) {
         if (uint8_t* d = mapped_range(h->base, host_span(h)))
             return run_mapped(host_items(h), [&](HostEngine&, hipStream_t st) {
                 return draid::launch_encode_strided(k, m, S, h->nstripes, d, h->strip_stride,
                                                     h->stripe_stride, st);
             });
+        if (is_pageable(h))
+            return run_bounce(h, nullptr);
+    }
     return run_chunks(
         h, chunk_stripes, 0, k,
         [&](Stage& s, uint32_t, uint32_t rows) {
@@ -322,6 +458,8 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
                                                          h->strip_stride, h->stripe_stride,
                                                          eng.zfail, nullptr, st);
             });
+    if (!(h->flags & DRAID_EC_HOST_STAGED) && is_pageable(h))
+        return run_bounce(h, fail);
     return run_chunks(
         h, chunk_stripes, 0, n,
         [&](Stage& s, uint32_t c0, uint32_t rows) {

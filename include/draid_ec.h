@@ -319,11 +319,15 @@ int draid_ec_ctx_set_autoflush(draid_ec_ctx *ctx, uint64_t segments);
  * SPDK's stripe buffers are host hugepages.  When the whole range is pinned or
  * registered (draid_ec_host_register) the kernel reads the strips it needs in
  * place over PCIe and writes P/Q (or the rebuilt strips) straight back: one
- * launch, no staging -- a reconstruct moves only the surviving strips.  For
- * pageable memory, or with flags = DRAID_EC_HOST_STAGED, the calls copy the
- * input strips in (hipMemcpy2DAsync per strip index over a chunk of stripes),
- * run the kernel in HBM and copy the results back, pipelined over three
- * streams; chunk_stripes = stripes per pipeline stage (0 = 64).  Synchronous.
+ * launch, no staging -- a reconstruct moves only the surviving strips.  With
+ * flags = DRAID_EC_HOST_STAGED (or host memory the runtime knows that is not one
+ * mapping) the calls copy the input strips in (hipMemcpy2DAsync per strip
+ * index over a chunk of stripes), run the kernel in HBM and copy the results
+ * back, pipelined over three streams; chunk_stripes = stripes per pipeline
+ * stage (0 = 64).  Pageable memory is bounced through two pinned buffers by the
+ * calling thread itself (the runtime's strided copies of pageable memory run at
+ * a quarter of that): only the strips the kernel reads go in, only the strips
+ * it wrote come out.  Synchronous.
  * ---------------------------------------------------------------------- */
 
 #define DRAID_EC_HOST_STAGED 1u
