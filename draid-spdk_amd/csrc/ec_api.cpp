@@ -8,6 +8,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -88,6 +89,14 @@ struct Scratch {
 // Calls that stage more than this go through the device arena (the copies then run at the
 // runtime's pageable rate either way, and pinned memory is not for hoarding).
 constexpr size_t kBounceMax = 8u << 20;
+size_t bounce_max()
+{
+    static const size_t v = [] {
+        const char* e = getenv("DRAID_EC_BOUNCE_MAX");  // bytes; A/B runs
+        return e ? static_cast<size_t>(strtoull(e, nullptr, 0)) : kBounceMax;
+    }();
+    return v;
+}
 thread_local draid::PerDevice<Scratch> t_scratch_of;
 
 // The calling thread's scratch on its current GPU; null (with the error
@@ -166,7 +175,7 @@ struct Vectors {
         Scratch* sc = scratch();
         if (!sc)
             return -1;
-        if (need <= kBounceMax) {
+        if (need <= bounce_max()) {
             if (sc->bounce_bytes < need) {
                 if (sc->bounce)
                     (void)hipHostFree(sc->bounce);
