@@ -44,6 +44,19 @@ def test_c_harness_gpu(ec):
     assert "PASS" in out.stdout
 
 
+@pytest.mark.gpu
+def test_pageable_memory_through_the_c_abi(ec):
+    """tests/c/test_pageable.c: malloc'd vectors through the isa-l-shaped calls on both
+    sides of the pinned-arena limit, and malloc'd strided stripes (with gaps, partial last
+    chunks, mixed failure tables) through draid_ec_host_encode / _reconstruct, bit-exact
+    against the oracle."""
+    _build()
+    out = subprocess.run([os.path.join(HERE, "c", "test_pageable")], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "PASS pageable" in out.stdout
+
+
 def test_c_sanitizers():
     """The host code under sanitizers.  The host RAID layer and
     stripe cache (compiled from source into the harness) under ASan + UBSan

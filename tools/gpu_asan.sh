@@ -24,6 +24,9 @@ timeout -k 10 120 tests/c/sg_bench_asan_gpu 4096 512 3 0 1024 >> $L 2>&1 || { ta
 # batch at 1 KiB iovecs x 1024 stripes), alone and with autoflush launching between them
 timeout -k 10 180 tests/c/sg_bench_asan_gpu 1024 1024 2 0 >> $L 2>&1 || { tail -40 $L; exit 1; }
 timeout -k 10 180 tests/c/sg_bench_asan_gpu 1024 1024 2 0 30000 >> $L 2>&1 || { tail -40 $L; exit 1; }
+# pageable memory: the pinned bounce arena and the device arena of the isa-l-shaped calls,
+# and host stripes bounced through pinned buffers by the calling thread
+timeout -k 10 300 tests/c/test_pageable_asan_gpu >> $L 2>&1 || { tail -40 $L; exit 1; }
 grep -c "AddressSanitizer" $L && exit 1
 grep -c "^PASS" $L
 tail -12 $L
