@@ -599,7 +599,7 @@ void drop_staged(draid_ec_ctx* c, Group& g, size_t keep)
 // descriptors into the next pinned ring slot and DMA them on the copy stream.
 // `perm` (may be null): segment i of the group is g's segment perm[i].
 // `ahead`: called from a queueing call -- never waits for a slot still in use
-// (returns 1 and stages nothing).
+// (returns kSlotBusy and stages nothing).
 int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size_t s1, bool ahead,
                 Staged* out)
 {
@@ -705,12 +705,10 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
         memcpy(h + o_len, lenp, nseg * sizeof(uint32_t));
     if (!work.empty())
         memcpy(h + o_work, work.data(), work.size() * sizeof(uint32_t));
-    // DMA the piece's descriptors: in address order the pointer table comes
-    // straight from the group's pinned storage, the rest (lengths, failure
-    // pairs, work list; none for uniform encode segments) from the slot.
-    // (Reading them in place from pinned memory instead was measured slower:
-    // 1.39 vs 1.00 ms for 4096 stripes of 4 KiB iovecs -- the per-item pointer
-    // loads then pay PCIe latency.)
+    // DMA the piece's descriptors: a piece in queue order takes its rows straight
+    // from the group's pinned storage and only the rest (lengths, update exponents,
+    // work list; none for uniform encode segments) from the slot; a piece in address
+    // order was packed into the slot row by row above and goes up in one copy.
     if (inplace)
         e = hipSuccess;
     else if (perm)
