@@ -334,8 +334,18 @@ int run_bounce(const draid_ec_host_stripes* h, const uint8_t* fail)
             const size_t s = static_cast<size_t>(c0) + r;
             if (fail && fail[2 * s] == DRAID_EC_FAIL_NONE && fail[2 * s + 1] == DRAID_EC_FAIL_NONE)
                 continue;  // nothing lost: the kernel skips the stripe, so nothing is read
+            // The kernel reads every surviving data strip, P whenever it survives, and Q
+            // only for a plan that needs the Q syndrome -- two data strips lost, or one and
+            // P (kern_reconstruct.hpp: useQ = needq && !lostQ).  A Q it has no use for
+            // stays where it is.
+            bool needQ = true;
+            if (fail) {
+                const uint32_t f0 = fail[2 * s], f1 = fail[2 * s + 1];
+                const uint32_t nd = (f0 < k ? 1u : 0u) + (f1 < k && f1 != f0 ? 1u : 0u);
+                needQ = nd == 2 || (nd == 1 && (f0 == k || f1 == k));
+            }
             for (uint32_t j = 0; j < n; ++j)
-                if (!written(c0 + r, j))
+                if (!written(c0 + r, j) && (j <= k || needQ))
                     memcpy(b.host + (static_cast<uint64_t>(r) * n + j) * S,
                            base + static_cast<uint64_t>(c0 + r) * h->stripe_stride +
                                j * h->strip_stride,
