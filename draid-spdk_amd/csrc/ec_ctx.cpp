@@ -103,9 +103,8 @@ struct Staged {
     bool uniform = false;           // every segment the same length: no work list
     bool inplace = false;           // the kernel reads the descriptors from the slot's pinned
                                     // host memory: nothing was uploaded
-    bool host_data = false;         // a small launch most of whose segments have strips in host
-                                    // memory: PCIe bound, better with few items resident
-                                    // (LaunchThrottle)
+    bool host_data = false;         // most of the segments have strips in host memory: PCIe
+                                    // bound, better with few items resident (LaunchThrottle)
     uint32_t nwork = 0, ulen = 0;   // work items; the uniform length
     size_t o_len = 0, o_fail = 0, o_work = 0;  // offsets into the slot
 };
@@ -728,7 +727,7 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     size_t host_segs = 0;
     for (size_t i = 0; i < nseg; ++i)
         host_segs += g.host[perm ? perm[s0 + i] : s0 + i];
-    out->host_data = 2 * host_segs > nseg && nwork64 <= draid::kThrottleItems;
+    out->host_data = 2 * host_segs > nseg;
     out->inplace = inplace;
     out->slot = si;
     out->s0 = s0;
@@ -753,7 +752,7 @@ int launch_piece(draid_ec_ctx* c, Group& g, const Staged& st)
         return ctx_fail(e, "descriptor upload event");
     const uint8_t* d = static_cast<const uint8_t*>(st.inplace ? sl.host_dev : sl.dev);
     // strips in host memory: a PCIe-bound launch runs faster with few items resident
-    draid::LaunchThrottle throttle(st.host_data);
+    draid::LaunchThrottle throttle(st.host_data, false);
     const auto* tab = reinterpret_cast<const uint8_t* const*>(d);
     const auto* lens = reinterpret_cast<const uint32_t*>(d + st.o_len);
     const void* wl = st.uniform ? nullptr : d + st.o_work;

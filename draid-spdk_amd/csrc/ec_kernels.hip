@@ -67,6 +67,19 @@ int get_variant() { return g_variant; }
 // together -- the fewer are resident, the less.
 thread_local uint32_t t_launch_lds = 0;
 static inline uint32_t launch_lds() { return t_launch_lds; }
+// The segment work lists have a better way to the same end: every one of their kernels
+// exists in a form that loops over the work items (one wave per item), so a launch on
+// host memory takes one workgroup per CU and no more, whatever the number of items.
+// Nothing is dispatched again while the launch runs, every wave keeps its own loads in
+// flight from its first item to its last, and the link stays busy: B 8+2 x 64 KiB
+// stripes in pinned memory through a context, us per flush and wait, this form against
+// shared items held to one per CU by LDS: B = 16 176 vs 197 (encode) and 177 vs 202
+// (dual reconstruct), 32: 326 vs 375, 64: 622 vs 652, 256: 2443 vs 2536, 1024: 9486 vs
+// 9806 (tools/pcie_grid_probe.py; 512 workgroups the same to 1%, 128 and 1024 2-4%
+// behind, 64 and fewer as slow as no bound at all).  On stripes in HBM the same form
+// costs a factor of several, so only launches inside a LaunchThrottle take it.
+thread_local bool t_host_work = false;
+static inline bool host_work() { return t_host_work; }
 // One item per CU (8+2 x 64 KiB stripes in pinned memory, us per launch of B stripes, no
 // extra LDS / 56 KiB (two items per CU) / 128 KiB (one): B = 16 203 / 184 / 170, 32: 372 /
 // 344 / 321, 64: 675 / 657 / 634, 256: 2478 / 2482 / 2423, 1024 the same; the dual
@@ -92,12 +105,19 @@ static uint32_t throttle_bytes()
     }();
     return bytes;
 }
-LaunchThrottle::LaunchThrottle(bool on) : prev_(t_launch_lds)
+LaunchThrottle::LaunchThrottle(bool on, bool lds) : prev_(t_launch_lds), prev_work_(t_host_work)
 {
-    if (on)
-        t_launch_lds = throttle_bytes();
+    if (on) {
+        t_host_work = true;
+        if (lds)
+            t_launch_lds = throttle_bytes();
+    }
 }
-LaunchThrottle::~LaunchThrottle() { t_launch_lds = prev_; }
+LaunchThrottle::~LaunchThrottle()
+{
+    t_launch_lds = prev_;
+    t_host_work = prev_work_;
+}
 // Test / measurement hook (not in the public header): dynamic LDS on every later
 // launch of the calling thread.
 extern "C" void draid_ec_test_launch_lds(uint32_t bytes) { t_launch_lds = bytes; }
@@ -135,7 +155,7 @@ static inline uint32_t chunks_per_stripe(uint64_t len, int nthr, int U)
     return static_cast<uint32_t>(c == 0 ? 1 : c);
 }
 
-[[maybe_unused]] static int device_cus()
+static int device_cus()
 {
     static thread_local int dev = -1, cus = 0;
     int d = 0;
@@ -147,6 +167,15 @@ static inline uint32_t chunks_per_stripe(uint64_t len, int nthr, int U)
         dev = d;
     }
     return cus;
+}
+
+// Workgroups of a work-list launch on host memory: one per CU.  DRAID_EC_HOST_GRID
+// overrides (A/B runs; 0 = one per work item, the looping form then never loops).
+static uint32_t host_grid(uint32_t nwork)
+{
+    static const long env = getenv("DRAID_EC_HOST_GRID") ? atol(getenv("DRAID_EC_HOST_GRID")) : -1;
+    const uint32_t cap = env < 0 ? static_cast<uint32_t>(device_cus()) : static_cast<uint32_t>(env);
+    return cap > 0 && cap < nwork ? cap : nwork;
 }
 
 template <class C>
@@ -666,6 +695,21 @@ static hipError_t go_encode_work(const uint8_t* const* tab, uint32_t k, uint32_t
     if (nwork == 0)
         return hipSuccess;
     const RowOffs rows{reinterpret_cast<const uint8_t*>(tab), row_bytes};
+    if (host_work()) {
+        // strips in host memory: the looping one-wave form, one workgroup per CU
+        using C1 = std::conditional_t<(C::SPLIT > 1), EncCfg<C::U, 0, enc_waves(KT), 1>, C>;
+        static_assert(C1::ITEM * C1::U == C::ITEM * C::U, "the host counted items of this size");
+        const uint32_t grid = host_grid(nwork);
+        if (row_bytes)
+            hipLaunchKernelGGL((k_encode_work<KT, M, false, C1, RowOffs>), dim3(grid),
+                               dim3(C1::NTHR), 0, st, rows, k, work_src<C1>(seg_len, work, ulen),
+                               nwork);
+        else
+            hipLaunchKernelGGL((k_encode_work<KT, M, false, C1>), dim3(grid), dim3(C1::NTHR), 0, st,
+                               WorkEncPtrs<KT>{tab, k + M}, k, work_src<C1>(seg_len, work, ulen),
+                               nwork);
+        return hipGetLastError();
+    }
     if constexpr (C::SPLIT > 1) {
         if (row_bytes)
             hipLaunchKernelGGL((k_encode_work_split<KT, M, C, RowOffs>), dim3(nwork),
@@ -696,6 +740,21 @@ static hipError_t go_reconstruct_work(const uint8_t* const* tab, uint32_t tstrid
     if (nwork == 0)
         return hipSuccess;
     const RowOffs rows{reinterpret_cast<const uint8_t*>(tab), row_bytes};
+    if (host_work()) {
+        // strips in host memory: the looping one-wave form, one workgroup per CU
+        using C1 = std::conditional_t<(C::SPLIT > 1), RecCfg<C::U, rec_waves(KT, M), 1>, C>;
+        static_assert(C1::ITEM * C1::U == C::ITEM * C::U, "the host counted items of this size");
+        const uint32_t grid = host_grid(nwork);
+        if (row_bytes)
+            hipLaunchKernelGGL((k_reconstruct_work<KT, M, C1, RowOffs>), dim3(grid), dim3(C1::NTHR),
+                               0, st, rows, k, work_src<C1>(seg_len, work, ulen), fail, fstride,
+                               nwork);
+        else
+            hipLaunchKernelGGL((k_reconstruct_work<KT, M, C1>), dim3(grid), dim3(C1::NTHR), 0, st,
+                               TablePtrs{tab, tstride}, k, work_src<C1>(seg_len, work, ulen), fail,
+                               fstride, nwork);
+        return hipGetLastError();
+    }
     if constexpr (C::SPLIT > 1) {
         if (row_bytes)
             hipLaunchKernelGGL((k_reconstruct_work_cols<KT, M, C, RowOffs>), dim3(nwork),
@@ -807,8 +866,12 @@ static hipError_t go_update_work(uint32_t nd, const uint8_t* const* table, const
 {
     using C = EncCfg<1, 0, DRAID_UPD_WAVES>;  // buffer nt loads, write-through nt stores
     const WorkSrc ws = work_src<C>(seg_len, work, ulen);
-    hipLaunchKernelGGL((k_update_work<M, NDT, C>), dim3(nwork), dim3(C::NTHR), launch_lds(), st, table, nd,
-                       exps, ws, nwork);
+    if (host_work())
+        hipLaunchKernelGGL((k_update_work<M, NDT, C, true>), dim3(host_grid(nwork)), dim3(C::NTHR), 0,
+                           st, table, nd, exps, ws, nwork);
+    else
+        hipLaunchKernelGGL((k_update_work<M, NDT, C>), dim3(nwork), dim3(C::NTHR), launch_lds(), st,
+                           table, nd, exps, ws, nwork);
     return hipGetLastError();
 }
 

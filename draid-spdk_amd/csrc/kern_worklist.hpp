@@ -161,15 +161,12 @@ __device__ __forceinline__ uint32_t load_const_byte(const uint8_t* a, size_t idx
 }
 
 template <int M, int NDT, class C>
-__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_update_work(
-    const uint8_t* const* tab, uint32_t nd_rt, const uint8_t* exps, WorkSrc ws, uint32_t nwork)
+__device__ __forceinline__ void update_item(const uint8_t* const* tab, uint32_t nd_rt,
+                                            const uint8_t* exps, const WorkSrc& ws, uint32_t b)
 {
     constexpr uint32_t EPB = static_cast<uint32_t>(C::NTHR) * C::U;
     static_assert(C::U == 1, "one vector per lane");
     const uint32_t nd = NDT > 0 ? NDT : nd_rt;
-    const uint32_t b = blockIdx.x;  // one work item per workgroup
-    if (b >= nwork)
-        return;
     uint32_t seg, chunk, len, cps;
     ws.get(b, EPB * 16, seg, chunk, len, cps);
     const TablePtrs row{tab, 2 * nd + M};
@@ -235,6 +232,21 @@ __global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_update_work(
         const uint32_t b1 = min(len, (chunk + 1) * EPB * 16);
         for (uint32_t i = chunk * EPB * 16 + threadIdx.x; i < b1; i += C::NTHR)
             body(uint32_t{}, i);
+    }
+}
+
+// LOOP == false: one work item per workgroup.  LOOP == true: a grid-stride loop, for
+// launches with fewer workgroups than items (strips in host memory, ec_kernels.hip).
+template <int M, int NDT, class C, bool LOOP = false>
+__global__ __launch_bounds__(C::NTHR) DRAID_WAVES_PER_EU(C) void k_update_work(
+    const uint8_t* const* tab, uint32_t nd_rt, const uint8_t* exps, WorkSrc ws, uint32_t nwork)
+{
+    if constexpr (LOOP) {
+        for (uint32_t b = blockIdx.x; b < nwork; b += gridDim.x)
+            update_item<M, NDT, C>(tab, nd_rt, exps, ws, b);
+    } else {
+        if (blockIdx.x < nwork)
+            update_item<M, NDT, C>(tab, nd_rt, exps, ws, blockIdx.x);
     }
 }
 
