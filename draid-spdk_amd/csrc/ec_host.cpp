@@ -192,11 +192,6 @@ uint8_t* mapped_range(const void* p, uint64_t span)
     return d1 == d0 + (span - 1) ? d0 : nullptr;
 }
 
-uint64_t host_items(const draid_ec_host_stripes* h)
-{
-    return (h->strip_len + draid::kItemBytes - 1) / draid::kItemBytes * h->nstripes;
-}
-
 uint64_t host_span(const draid_ec_host_stripes* h)
 {
     return static_cast<uint64_t>(h->nstripes - 1) * h->stripe_stride +
@@ -205,7 +200,7 @@ uint64_t host_span(const draid_ec_host_stripes* h)
 
 // In-place path over mapped host stripes: one launch, then wait.
 template <class Launch>
-int run_mapped(uint64_t items, Launch&& launch)
+int run_mapped(Launch&& launch)
 {
     HostEngine& eng = engine();
     Stage& s = eng.st[0];
@@ -213,8 +208,8 @@ int run_mapped(uint64_t items, Launch&& launch)
     if (!s.stream && (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
         return draid::fail_hip(e, "hipStreamCreate(host engine)");
     {
-        // every strip crosses PCIe: a small launch runs faster with few items resident
-        draid::LaunchThrottle throttle(items <= draid::kThrottleItems);
+        // every strip crosses PCIe: the launch runs faster with few items resident
+        draid::LaunchThrottle throttle(true, false);
         e = launch(eng, s.stream);
     }
     if (e != hipSuccess)
@@ -277,7 +272,7 @@ int run_bounce(const draid_ec_host_stripes* h, const uint8_t* fail)
     const uint64_t S = h->strip_len;
     const uint64_t stripe_bytes = n * S;
     // chunks of about 16 MiB: small enough for the copies of one to hide behind the
-    // kernel of another, small enough to run throttled (LaunchThrottle)
+    // kernel of another
     const uint32_t chunk = static_cast<uint32_t>(
         std::min<uint64_t>(h->nstripes, std::max<uint64_t>(1, (16u << 20) / stripe_bytes)));
     const size_t need = static_cast<size_t>(chunk) * stripe_bytes + 2 * static_cast<size_t>(chunk);
@@ -351,8 +346,7 @@ int run_bounce(const draid_ec_host_stripes* h, const uint8_t* fail)
                                j * h->strip_stride,
                            S);
         }
-        const uint64_t items = (S + draid::kItemBytes - 1) / draid::kItemBytes * b.rows;
-        draid::LaunchThrottle throttle(items <= draid::kThrottleItems);
+        draid::LaunchThrottle throttle(true, false);
         if (fail) {
             uint8_t* f = b.host + static_cast<size_t>(chunk) * stripe_bytes;
             memcpy(f, fail + 2 * static_cast<size_t>(c0), 2 * static_cast<size_t>(b.rows));
@@ -396,7 +390,7 @@ int draid_ec_host_encode(const draid_ec_host_stripes* h, uint32_t chunk_stripes)
     const uint64_t S = h->strip_len;
     if (!(h->flags & DRAID_EC_HOST_STAGED)) {
         if (uint8_t* d = mapped_range(h->base, host_span(h)))
-            return run_mapped(host_items(h), [&](HostEngine&, hipStream_t st) {
+            return run_mapped([&](HostEngine&, hipStream_t st) {
                 return draid::launch_encode_strided(k, m, S, h->nstripes, d, h->strip_stride,
                                                     h->stripe_stride, st);
             });
@@ -449,7 +443,7 @@ int draid_ec_host_reconstruct(const draid_ec_host_stripes* h, const uint8_t* fai
     }
     if (!(h->flags & DRAID_EC_HOST_STAGED))
         if (uint8_t* d = mapped_range(h->base, host_span(h)))
-            return run_mapped(host_items(h), [&](HostEngine& eng, hipStream_t st) {
+            return run_mapped([&](HostEngine& eng, hipStream_t st) {
                 const size_t fb = 2 * static_cast<size_t>(h->nstripes);
                 hipError_t e;
                 if (eng.zfail_bytes < fb) {

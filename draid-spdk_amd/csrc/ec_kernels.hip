@@ -213,57 +213,6 @@ static inline dim3 split_grid(uint32_t cps, uint32_t nstripes, ItemGrid& ig)
     return dim3(cps << ig.fold, ny, (rows + kGridY - 1) / kGridY);
 }
 
-template <int KT, int M, bool CHECK, class C, class Ptrs>
-static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
-                            uint32_t* flag, hipStream_t st)
-{
-    uint32_t cps, grid;
-    if (nstripes == 0 || len == 0)
-        return hipSuccess;
-    if (!grid_for<C>(len, nstripes, cps, grid))
-        return hipErrorInvalidValue;
-    if constexpr (C::SPLIT > 1) {
-        ItemGrid ig;
-        const dim3 g = split_grid(cps, nstripes, ig);
-        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
-                           static_cast<uint32_t>(len), cps, nstripes, flag, ig);
-    } else if constexpr (KT > 0 && std::is_same<Ptrs, TablePtrs>::value)
-        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), launch_lds(),
-                           st, TablePlain{pp.tab, pp.stride}, k, static_cast<uint32_t>(len), cps,
-                           nstripes, flag);
-    else
-        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
-                           k, static_cast<uint32_t>(len), cps, nstripes, flag);
-    return hipGetLastError();
-}
-
-// BYSTRIP: a shared item's arithmetic is dealt by strip (k_reconstruct_split)
-// instead of by column (k_reconstruct_cols).
-template <int KT, int M, class C, bool BYSTRIP = false, class Ptrs>
-static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
-                                 const uint8_t* fail, uint32_t f01, uint32_t* bad, hipStream_t st)
-{
-    uint32_t cps, grid;
-    if (nstripes == 0 || len == 0)
-        return hipSuccess;
-    if (!grid_for<C>(len, nstripes, cps, grid))
-        return hipErrorInvalidValue;
-    if constexpr (C::SPLIT > 1) {
-        ItemGrid ig;
-        const dim3 g = split_grid(cps, nstripes, ig);
-        if constexpr (BYSTRIP)
-            hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
-                               static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
-        else
-            hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
-                               static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
-    } else {
-        hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
-                           k, static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
-    }
-    return hipGetLastError();
-}
-
 // Production configuration: one wave (64 lanes) per workgroup, non-temporal
 // loads and stores, one item per workgroup, LDS-staged GF tables.  A one-wave
 // item is 1 KiB of every strip of a stripe.  Measured against 256 lanes
@@ -455,6 +404,83 @@ using CfgDefault = Cfg<kLanes, U, 3, 0, 0>;  // read-modify-write update: global
 // strided layouts); the scatter-gather lists run them through the run-time loop.
 #define DRAID_FOR_EACH_WIDE_K(X) \
     X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+
+template <int KT, int M, bool CHECK, class C, class Ptrs>
+static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
+                            uint32_t* flag, hipStream_t st)
+{
+    uint32_t cps, grid;
+    if (nstripes == 0 || len == 0)
+        return hipSuccess;
+    if (!grid_for<C>(len, nstripes, cps, grid))
+        return hipErrorInvalidValue;
+    if constexpr (std::is_same<Ptrs, StridedPtrs>::value && !CHECK) {
+        if (host_work()) {
+            // stripes in host memory (ec_host.cpp): the looping one-wave form, one workgroup
+            // per CU, as for the work lists; widths above 20 through the run-time loop
+            constexpr int K1 = KT > 20 ? 0 : KT;
+            using C1 = EncCfg<C::ITEM * C::U / 64, 2, K1 ? enc_waves(K1) : DRAID_RT_ENC_WAVES, 1>;
+            static_assert(C1::ITEM * C1::U == C::ITEM * C::U, "same items");
+            hipLaunchKernelGGL((k_encode<K1, M, false, C1, Ptrs>), dim3(host_grid(cps * nstripes)),
+                               dim3(C1::NTHR), 0, st, pp, k, static_cast<uint32_t>(len), cps,
+                               nstripes, flag);
+            return hipGetLastError();
+        }
+    }
+    if constexpr (C::SPLIT > 1) {
+        ItemGrid ig;
+        const dim3 g = split_grid(cps, nstripes, ig);
+        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
+                           static_cast<uint32_t>(len), cps, nstripes, flag, ig);
+    } else if constexpr (KT > 0 && std::is_same<Ptrs, TablePtrs>::value)
+        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), launch_lds(),
+                           st, TablePlain{pp.tab, pp.stride}, k, static_cast<uint32_t>(len), cps,
+                           nstripes, flag);
+    else
+        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
+                           k, static_cast<uint32_t>(len), cps, nstripes, flag);
+    return hipGetLastError();
+}
+
+// BYSTRIP: a shared item's arithmetic is dealt by strip (k_reconstruct_split)
+// instead of by column (k_reconstruct_cols).
+template <int KT, int M, class C, bool BYSTRIP = false, class Ptrs>
+static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
+                                 const uint8_t* fail, uint32_t f01, uint32_t* bad, hipStream_t st)
+{
+    uint32_t cps, grid;
+    if (nstripes == 0 || len == 0)
+        return hipSuccess;
+    if (!grid_for<C>(len, nstripes, cps, grid))
+        return hipErrorInvalidValue;
+    if constexpr (std::is_same<Ptrs, StridedPtrs>::value) {
+        if (host_work()) {
+            // stripes in host memory: the looping one-wave form, as in go_encode
+            constexpr int K1 = KT > 20 ? 0 : KT;
+            using C1 = Cfg<64, C::ITEM * C::U / 64, pol_aux(DRAID_REC_LOAD_AUX, 18), 2, 0,
+                           K1 ? rec_waves(K1, M) : DRAID_RT_REC_WAVES, 1>;
+            static_assert(C1::ITEM * C1::U == C::ITEM * C::U, "same items");
+            hipLaunchKernelGGL((k_reconstruct<K1, M, C1, Ptrs>), dim3(host_grid(cps * nstripes)),
+                               dim3(C1::NTHR), 0, st, pp, k, static_cast<uint32_t>(len), cps,
+                               nstripes, fail, f01, bad);
+            return hipGetLastError();
+        }
+    }
+    if constexpr (C::SPLIT > 1) {
+        ItemGrid ig;
+        const dim3 g = split_grid(cps, nstripes, ig);
+        if constexpr (BYSTRIP)
+            hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
+                               static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
+        else
+            hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
+                               static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
+    } else {
+        hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
+                           k, static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
+    }
+    return hipGetLastError();
+}
 
 template <int M, class Ptrs>
 static hipError_t dispatch_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t nstripes,
