@@ -104,7 +104,7 @@ struct Staged {
     bool inplace = false;           // the kernel reads the descriptors from the slot's pinned
                                     // host memory: nothing was uploaded
     bool host_data = false;         // most of the segments have strips in host memory: PCIe
-                                    // bound, better with few items resident (LaunchThrottle)
+                                    // bound, better with few items resident (HostLaunch)
     uint32_t nwork = 0, ulen = 0;   // work items; the uniform length
     size_t o_len = 0, o_fail = 0, o_work = 0;  // offsets into the slot
 };
@@ -752,7 +752,7 @@ int launch_piece(draid_ec_ctx* c, Group& g, const Staged& st)
         return ctx_fail(e, "descriptor upload event");
     const uint8_t* d = static_cast<const uint8_t*>(st.inplace ? sl.host_dev : sl.dev);
     // strips in host memory: a PCIe-bound launch runs faster with few items resident
-    draid::LaunchThrottle throttle(st.host_data, false);
+    draid::HostLaunch host(st.host_data);
     const auto* tab = reinterpret_cast<const uint8_t* const*>(d);
     const auto* lens = reinterpret_cast<const uint32_t*>(d + st.o_len);
     const void* wl = st.uniform ? nullptr : d + st.o_work;

@@ -209,7 +209,7 @@ int run_mapped(Launch&& launch)
         return draid::fail_hip(e, "hipStreamCreate(host engine)");
     {
         // every strip crosses PCIe: the launch runs faster with few items resident
-        draid::LaunchThrottle throttle(true, false);
+        draid::HostLaunch host(true);
         e = launch(eng, s.stream);
     }
     if (e != hipSuccess)
@@ -346,7 +346,7 @@ int run_bounce(const draid_ec_host_stripes* h, const uint8_t* fail)
                                j * h->strip_stride,
                            S);
         }
-        draid::LaunchThrottle throttle(true, false);
+        draid::HostLaunch host(true);
         if (fail) {
             uint8_t* f = b.host + static_cast<size_t>(chunk) * stripe_bytes;
             memcpy(f, fail + 2 * static_cast<size_t>(c0), 2 * static_cast<size_t>(b.rows));

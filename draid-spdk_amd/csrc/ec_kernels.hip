@@ -58,68 +58,37 @@ static int g_variant = 0;
 void set_variant(int v) { g_variant = DRAID_EC_LAB ? v : 0; }
 int get_variant() { return g_variant; }
 
-// Dynamic LDS added to every launch of the calling thread while a LaunchThrottle is
-// alive.  No kernel uses it: LDS a workgroup holds is LDS its CU cannot give to
-// another, so it bounds how many items are resident per CU without a second
-// instance of any kernel.  Launches whose strips live in HOST memory want that:
-// every resident item has all its reads queued on the PCIe link at once, and a
-// launch of a few dozen stripes pays for the last generation of items draining
-// together -- the fewer are resident, the less.
-thread_local uint32_t t_launch_lds = 0;
-static inline uint32_t launch_lds() { return t_launch_lds; }
-// The segment work lists have a better way to the same end: every one of their kernels
-// exists in a form that loops over the work items (one wave per item), so a launch on
-// host memory takes one workgroup per CU and no more, whatever the number of items.
-// Nothing is dispatched again while the launch runs, every wave keeps its own loads in
-// flight from its first item to its last, and the link stays busy: B 8+2 x 64 KiB
-// stripes in pinned memory through a context, us per flush and wait, this form against
-// shared items held to one per CU by LDS: B = 16 176 vs 197 (encode) and 177 vs 202
-// (dual reconstruct), 32: 326 vs 375, 64: 622 vs 652, 256: 2443 vs 2536, 1024: 9486 vs
-// 9806 (tools/pcie_grid_probe.py; 512 workgroups the same to 1%, 128 and 1024 2-4%
-// behind, 64 and fewer as slow as no bound at all).  On stripes in HBM the same form
-// costs a factor of several, so only launches inside a LaunchThrottle take it.
+// Launches on strips in HOST memory (inside a HostLaunch scope) want few items
+// resident: every resident item has all its reads queued on the PCIe link at once,
+// workgroups that come and go leave gaps in that queue, and a launch of a few dozen
+// stripes pays for the last generation of items draining together.  Every kernel that
+// can see host memory therefore has a form that loops over its items -- one wave per
+// item, a grid-stride loop -- and such a launch takes one workgroup per CU and no more,
+// whatever the number of items.  Nothing is dispatched again while the launch runs,
+// every wave keeps its own loads in flight from its first item to its last, and the
+// link stays busy.  B 8+2 x 64 KiB stripes in pinned memory through a context, us per
+// flush and wait, against items shared by four waves, one workgroup per item, held to
+// one per CU (by dynamic LDS that no kernel used: the form before this one) and against
+// the same with no bound: B = 16 176 vs 197 vs 202 (encode), 177 vs 202 vs 212 (dual
+// reconstruct); 32: 326 vs 375 vs 371; 64: 622 vs 652 vs 652; 256: 2443 vs 2536 vs
+// 2518; 1024: 9486 vs 9806 vs 9819 (tools/pcie_grid_probe.py; 512 workgroups the same
+// to 1%, 128 and 1024 2-4% behind, 64 and fewer as slow as no bound at all).  On stripes
+// in HBM the looping form costs a factor of several, so only launches inside a
+// HostLaunch take it.
 thread_local bool t_host_work = false;
 static inline bool host_work() { return t_host_work; }
-// One item per CU (8+2 x 64 KiB stripes in pinned memory, us per launch of B stripes, no
-// extra LDS / 56 KiB (two items per CU) / 128 KiB (one): B = 16 203 / 184 / 170, 32: 372 /
-// 344 / 321, 64: 675 / 657 / 634, 256: 2478 / 2482 / 2423, 1024 the same; the dual
-// reconstruct alike.  The same LDS on stripes in HBM costs a factor of four, and launches
-// much larger than the CUs hold at once lose a few per cent to it: kThrottleItems.)
-constexpr int kThrottleLds = 128 * 1024;
-static uint32_t throttle_bytes()
+HostLaunch::HostLaunch(bool on) : prev_(t_host_work)
 {
-    // once per thread and device would be exact; one query serves: every GPU of a node is
-    // the same part.  DRAID_EC_THROTTLE_LDS (bytes, 0 = off) overrides, for A/B runs.
-    static const uint32_t bytes = [] {
-        if (const char* e = getenv("DRAID_EC_THROTTLE_LDS"))
-            return static_cast<uint32_t>(strtoul(e, nullptr, 0));
-        int dev = 0, max_block = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&max_block, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) !=
-                hipSuccess)
-            return 0u;
-        // room left for the largest static allocation of any kernel here (the column
-        // reconstruct's k + 2 rows of 1 KiB at k = 20)
-        const int room = max_block - 24 * 1024;
-        return static_cast<uint32_t>(room > kThrottleLds ? kThrottleLds : room > 0 ? room : 0);
-    }();
-    return bytes;
-}
-LaunchThrottle::LaunchThrottle(bool on, bool lds) : prev_(t_launch_lds), prev_work_(t_host_work)
-{
-    if (on) {
+    if (on)
         t_host_work = true;
-        if (lds)
-            t_launch_lds = throttle_bytes();
-    }
 }
-LaunchThrottle::~LaunchThrottle()
-{
-    t_launch_lds = prev_;
-    t_host_work = prev_work_;
-}
-// Test / measurement hook (not in the public header): dynamic LDS on every later
-// launch of the calling thread.
+HostLaunch::~HostLaunch() { t_host_work = prev_; }
+// Measurement hook (not in the public header; tools/pcie_throttle_probe.py): dynamic
+// LDS, which no kernel uses, on every later launch of the calling thread -- LDS a
+// workgroup holds is LDS its CU cannot give to another, so it bounds the items resident
+// per CU.
+thread_local uint32_t t_launch_lds = 0;
+static inline uint32_t launch_lds() { return t_launch_lds; }
 extern "C" void draid_ec_test_launch_lds(uint32_t bytes) { t_launch_lds = bytes; }
 
 // ------------------------------------------------------------ launchers

@@ -106,26 +106,17 @@ int translate(const void* p, size_t len, const void** dev, int on_device = kCurr
 void translate_invalidate();
 
 // While one is alive (and `on`), the launches of the calling thread are launches on
-// strips in HOST memory, which run faster with few items resident (ec_kernels.hip):
-// the segment work lists (launch_*_work) run their looping form, one workgroup per CU,
-// at every size; the other kernels, which have no such form, carry dynamic LDS that
-// bounds the items resident per CU when `lds` is set.  The LDS pays for launches of up
-// to about kThrottleItems work items (1 KiB chunks of a stripe) -- the raid module over
-// null base bdevs, MiB/s with and without it when that was the work lists' bound too:
-// 8+2 x 64 KiB full-stripe writes at 16 requests per launch (1024 items) 41.4k vs 36.6k,
-// at 32 (2048 items) 44.0k vs 42.7k, at 64 (4096 items) 44.2k vs 46.4k; 16+2 x 256 KiB at
-// 16 per launch (4096 items) 46.5k vs 47.4k.
-constexpr uint64_t kThrottleItems = 2048;
-class LaunchThrottle {
+// strips in HOST memory: the segment work lists (launch_*_work) and the strided batches
+// (launch_*_strided) run their looping form, one workgroup per CU (ec_kernels.hip).
+class HostLaunch {
 public:
-    explicit LaunchThrottle(bool on, bool lds = true);
-    ~LaunchThrottle();
-    LaunchThrottle(const LaunchThrottle&) = delete;
-    LaunchThrottle& operator=(const LaunchThrottle&) = delete;
+    explicit HostLaunch(bool on);
+    ~HostLaunch();
+    HostLaunch(const HostLaunch&) = delete;
+    HostLaunch& operator=(const HostLaunch&) = delete;
 
 private:
-    uint32_t prev_;
-    bool prev_work_;
+    bool prev_;
 };
 
 // Variant selector for A/B experiments inside one process (0 = default).

@@ -1,8 +1,8 @@
-"""How a small launch on host memory depends on the workgroups resident at once: B RAID6
-8+2 x 64 KiB stripes in pinned host memory through a context (encode_sg, flush,
-synchronize), microseconds per flush.  With a lab library built with one wave per item
-(-DDRAID_ENC_SPLIT=1), whose work-list encode is a grid-stride loop, DRAID_LAB_GRID caps
-the grid: the same items run through fewer workgroups.  One JSON line."""
+"""How a launch on host memory depends on the workgroups it runs in: B RAID6 8+2 x 64 KiB
+stripes in pinned host memory through a host-pointer context (encode_sg / reconstruct_sg,
+flush, synchronize), microseconds per flush and wait.  Such launches run the work lists'
+looping kernels; DRAID_EC_HOST_GRID sets their workgroups (default: one per CU; 0: one per
+work item, so nothing loops).  One JSON line."""
 import json
 import os
 import sys
@@ -19,8 +19,7 @@ k, m, S = 8, 2, 65536
 n = k + m
 ec.lib()
 torch.cuda.init()
-out = {"grid": os.environ.get("DRAID_LAB_GRID", "all"),
-       "throttle": os.environ.get("DRAID_EC_THROTTLE_LDS", "default")}
+out = {"grid": os.environ.get("DRAID_EC_HOST_GRID", "CUs")}
 for B in (4, 16, 32, 64, 256, 1024):
     host = torch.empty(B * n * S, dtype=torch.uint8).pin_memory()
     host.view(B, n, S)[:, :k] = torch.randint(0, 256, (B, k, S), dtype=torch.uint8)
