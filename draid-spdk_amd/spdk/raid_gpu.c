@@ -75,7 +75,13 @@
  * smaller pieces: one batch computes while the next one grows, the GPU never
  * idles for lack of a queued launch, and a flush never has to wait for one of
  * the context's descriptor ring slots. */
+#ifndef RG_MAX_INFLIGHT
 #define RG_MAX_INFLIGHT 2
+#endif
+/* A launch takes at most 1 / RG_TAKE_DIV of the channel's busy requests. */
+#ifndef RG_TAKE_DIV
+#define RG_TAKE_DIV 2
+#endif
 #define RG_CACHE_STRIPES RAID_MAX_STRIPES
 
 enum rg_kind { RG_WRITE_FULL, RG_WRITE_PARTIAL, RG_WRITE_DEGRADED, RG_READ };
@@ -934,7 +940,7 @@ rg_poll(void *arg)
 		return busy ? SPDK_POLLER_BUSY : SPDK_POLLER_IDLE;
 	}
 	for (g = 0; g < info->ngpus; g++) {
-		const int take = spdk_max(1, (ch->busy_reqs + 1) / 2);
+		const int take = spdk_max(1, (ch->busy_reqs + RG_TAKE_DIV - 1) / RG_TAKE_DIV);
 		uint64_t ticket;
 		int rc, n = 0, i;
 
