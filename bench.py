@@ -214,7 +214,11 @@ def run_single_process(args, torch, ec) -> None:
     mg.synchronize()
     # per-kernel events on slot 0's stream (the stream its kernels are launched on)
     s0 = torch.cuda.ExternalStream(mg.stream(0), device=torch.device("cuda", devices[0]))
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # Two event records per step (before the encode, between the kernels); the record in
+    # front of step i+1 also ends step i's reconstruct -- a record between two kernels costs
+    # the stream a few microseconds, so none is made twice.
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    ev_end = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     for i in range(args.steps):
         # slot 0's kernels are bracketed by events; the other slots run the same step
@@ -401,7 +405,11 @@ def main() -> None:
         step()
     torch.cuda.synchronize(dev)
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # Two event records per step (before the encode, between the kernels); the record in
+    # front of step i+1 also ends step i's reconstruct -- a record between two kernels costs
+    # the stream a few microseconds, so none is made twice.
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    ev_end = torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -411,7 +419,7 @@ def main() -> None:
         ec.encode(batch, sh)
         ev[i][1].record(stream)
         ec.reconstruct(batch, fail, sh)
-        ev[i][2].record(stream)
+    ev_end.record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()  # this rank's K steps; the job's time is the max over ranks below
     if world > 1:
@@ -419,7 +427,8 @@ def main() -> None:
 
     elapsed = t1 - t0
     enc_all = [e[0].elapsed_time(e[1]) for e in ev]
-    rec_all = [e[1].elapsed_time(e[2]) for e in ev]
+    rec_all = [ev[i][1].elapsed_time(ev[i + 1][0] if i + 1 < args.steps else ev_end)
+               for i in range(args.steps)]
     enc_ms, rec_ms = float(np.mean(enc_all)), float(np.mean(rec_all))
     units = 2.0 * k * S * B * args.steps  # user-data bytes through both passes
     elapsed, units = reduce_timing(elapsed, units,
