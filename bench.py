@@ -226,12 +226,13 @@ def run_single_process(args, torch, ec) -> None:
         mg.encode(batches)
         ev[i][1].record(s0)
         mg.reconstruct(batches, fails)
-        ev[i][2].record(s0)
+    ev_end.record(s0)
     mg.synchronize()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    rec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    rec_ms = float(np.mean([ev[i][1].elapsed_time(ev[i + 1][0] if i + 1 < args.steps else ev_end)
+                            for i in range(args.steps)]))
     verified = None
     if not args.no_verify:
         # erase the failed data strips of every stripe on every slot, rebuild, compare
@@ -306,6 +307,9 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dispatch-events", action="store_true",
+                    help="time the kernels with events carried by each launch's own dispatch "
+                         "instead of events recorded on the stream around them")
     ap.add_argument("--layout", default="stripe_major", choices=["stripe_major", "strip_major"],
                     help="placement of the stripes in HBM: stripe-major (one stripe-cache slot per "
                          "stripe) or strip-major (one region per strip index)")
@@ -405,30 +409,54 @@ def main() -> None:
         step()
     torch.cuda.synchronize(dev)
 
-    # Two event records per step (before the encode, between the kernels); the record in
-    # front of step i+1 also ends step i's reconstruct -- a record between two kernels costs
-    # the stream a few microseconds, so none is made twice.
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
-    ev_end = torch.cuda.Event(enable_timing=True)
+    # Per-kernel HIP events over the timed region: recorded on the stream around the
+    # kernels, two per step (before the encode, between the kernels; the record in front of
+    # step i+1 also ends step i's reconstruct -- a record between two kernels costs the
+    # stream a few microseconds, 0.5% of this step, so none is made twice).
+    # --dispatch-events: every launch carries its own start and stop event in its dispatch
+    # instead (the runtime stamps them from the kernel's start and end): the durations are
+    # then the kernels' alone, as a profiler reports them (8+2 x 64 KiB: 384.6 + 399.4 us
+    # against 387.7 + 402.4 between records), but such a dispatch costs the stream more than
+    # a record does and the step runs 0.6% longer (0.7953 vs 0.7902 ms), so it is not the
+    # default.
+    if args.dispatch_events:
+        ev = [[ec.event_create() for _ in range(4)] for _ in range(args.steps)]
+    else:
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+        ev_end = torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        ec.encode(batch, sh)
-        ev[i][1].record(stream)
-        ec.reconstruct(batch, fail, sh)
-    ev_end.record(stream)
+    if args.dispatch_events:
+        for i in range(args.steps):
+            ec.launch_events(ev[i][0], ev[i][1])
+            ec.encode(batch, sh)
+            ec.launch_events(ev[i][2], ev[i][3])
+            ec.reconstruct(batch, fail, sh)
+    else:
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            ec.encode(batch, sh)
+            ev[i][1].record(stream)
+            ec.reconstruct(batch, fail, sh)
+        ev_end.record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()  # this rank's K steps; the job's time is the max over ranks below
     if world > 1:
         dist.barrier()
 
     elapsed = t1 - t0
-    enc_all = [e[0].elapsed_time(e[1]) for e in ev]
-    rec_all = [ev[i][1].elapsed_time(ev[i + 1][0] if i + 1 < args.steps else ev_end)
-               for i in range(args.steps)]
+    if args.dispatch_events:
+        enc_all = [ec.event_elapsed_ms(e[0], e[1]) for e in ev]
+        rec_all = [ec.event_elapsed_ms(e[2], e[3]) for e in ev]
+        for e in ev:
+            for x in e:
+                ec.event_destroy(x)
+    else:
+        enc_all = [e[0].elapsed_time(e[1]) for e in ev]
+        rec_all = [ev[i][1].elapsed_time(ev[i + 1][0] if i + 1 < args.steps else ev_end)
+                   for i in range(args.steps)]
     enc_ms, rec_ms = float(np.mean(enc_all)), float(np.mean(rec_all))
     units = 2.0 * k * S * B * args.steps  # user-data bytes through both passes
     elapsed, units = reduce_timing(elapsed, units,

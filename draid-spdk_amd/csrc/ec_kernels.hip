@@ -33,6 +33,7 @@
 // Workgroups are independent (no inter-workgroup communication, no atomics on
 // the hot path).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -90,6 +91,49 @@ HostLaunch::~HostLaunch() { t_host_work = prev_; }
 thread_local uint32_t t_launch_lds = 0;
 static inline uint32_t launch_lds() { return t_launch_lds; }
 extern "C" void draid_ec_test_launch_lds(uint32_t bytes) { t_launch_lds = bytes; }
+
+// Measurement hook (not in the public header; bench.py): the next batched launch of the
+// calling thread carries these two events in its own dispatch -- the runtime stamps them
+// from the kernel's start and end -- instead of the caller recording events around it.
+// An event recorded between two kernels is a packet of its own that costs the stream a
+// few microseconds; a step of two 0.4 ms kernels timed that way runs 0.5% longer per
+// record.
+thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+extern "C" void draid_ec_test_launch_events(void* start, void* stop)
+{
+    t_ev_start = static_cast<hipEvent_t>(start);
+    t_ev_stop = static_cast<hipEvent_t>(stop);
+}
+extern "C" int draid_ec_test_event_create(void** ev)
+{
+    hipEvent_t e = nullptr;
+    const hipError_t rc = hipEventCreate(&e);
+    *ev = e;
+    return rc == hipSuccess ? 0 : -1;
+}
+extern "C" int draid_ec_test_event_destroy(void* ev)
+{
+    return hipEventDestroy(static_cast<hipEvent_t>(ev)) == hipSuccess ? 0 : -1;
+}
+extern "C" int draid_ec_test_event_elapsed_ms(void* start, void* stop, float* ms)
+{
+    return hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+// A batched launch: plain, or with the pending events in its dispatch.
+template <class Kernel, class... Args>
+static void launch_batched(Kernel kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st,
+                           Args... args)
+{
+    if (t_ev_start || t_ev_stop) {
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, st, t_ev_start, t_ev_stop, 0, args...);
+        t_ev_start = t_ev_stop = nullptr;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+    }
+}
 
 // ------------------------------------------------------------ launchers
 
@@ -399,14 +443,14 @@ static hipError_t go_encode(const Ptrs& pp, uint32_t k, uint64_t len, uint32_t n
     if constexpr (C::SPLIT > 1) {
         ItemGrid ig;
         const dim3 g = split_grid(cps, nstripes, ig);
-        hipLaunchKernelGGL((k_encode_split<KT, M, CHECK, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
+        launch_batched(k_encode_split<KT, M, CHECK, C, Ptrs>, g, dim3(C::NTHR), launch_lds(), st, pp,
                            static_cast<uint32_t>(len), cps, nstripes, flag, ig);
     } else if constexpr (KT > 0 && std::is_same<Ptrs, TablePtrs>::value)
-        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, TablePlain>), dim3(grid), dim3(C::NTHR), launch_lds(),
+        launch_batched(k_encode<KT, M, CHECK, C, TablePlain>, dim3(grid), dim3(C::NTHR), launch_lds(),
                            st, TablePlain{pp.tab, pp.stride}, k, static_cast<uint32_t>(len), cps,
                            nstripes, flag);
     else
-        hipLaunchKernelGGL((k_encode<KT, M, CHECK, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
+        launch_batched(k_encode<KT, M, CHECK, C, Ptrs>, dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
                            k, static_cast<uint32_t>(len), cps, nstripes, flag);
     return hipGetLastError();
 }
@@ -439,13 +483,13 @@ static hipError_t go_reconstruct(const Ptrs& pp, uint32_t k, uint64_t len, uint3
         ItemGrid ig;
         const dim3 g = split_grid(cps, nstripes, ig);
         if constexpr (BYSTRIP)
-            hipLaunchKernelGGL((k_reconstruct_split<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
+            launch_batched(k_reconstruct_split<KT, M, C, Ptrs>, g, dim3(C::NTHR), launch_lds(), st, pp,
                                static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
         else
-            hipLaunchKernelGGL((k_reconstruct_cols<KT, M, C, Ptrs>), g, dim3(C::NTHR), launch_lds(), st, pp,
+            launch_batched(k_reconstruct_cols<KT, M, C, Ptrs>, g, dim3(C::NTHR), launch_lds(), st, pp,
                                static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad, ig);
     } else {
-        hipLaunchKernelGGL((k_reconstruct<KT, M, C, Ptrs>), dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
+        launch_batched(k_reconstruct<KT, M, C, Ptrs>, dim3(grid), dim3(C::NTHR), launch_lds(), st, pp,
                            k, static_cast<uint32_t>(len), cps, nstripes, fail, f01, bad);
     }
     return hipGetLastError();

@@ -165,6 +165,11 @@ def lib() -> C.CDLL:
         L.draid_ec_ctx_test_fail_after.restype = None
         L.draid_ec_ctx_test_staged.argtypes = [vp]
         L.draid_ec_ctx_test_staged.restype = i32
+        L.draid_ec_test_launch_events.argtypes = [vp, vp]
+        L.draid_ec_test_launch_events.restype = None
+        L.draid_ec_test_event_create.argtypes = [C.POINTER(vp)]
+        L.draid_ec_test_event_destroy.argtypes = [vp]
+        L.draid_ec_test_event_elapsed_ms.argtypes = [vp, vp, C.POINTER(C.c_float)]
         L.draid_ec_ctx_encode_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, C.c_size_t]
         L.draid_ec_ctx_reconstruct_sg.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp,
                                                   C.c_size_t, i32, vp]
@@ -176,6 +181,30 @@ def lib() -> C.CDLL:
         L.draid_ec_host_reconstruct.argtypes = [C.POINTER(HostStripes), vp, C.c_uint32]
         _lib = L
     return _lib
+
+
+# ---- measurement hooks (not part of the C ABI of the header) ----
+
+def event_create() -> int:
+    ev = C.c_void_p()
+    _check(lib().draid_ec_test_event_create(C.byref(ev)), "event_create")
+    return ev.value
+
+
+def event_destroy(ev: int) -> None:
+    lib().draid_ec_test_event_destroy(ev)
+
+
+def event_elapsed_ms(start: int, stop: int) -> float:
+    ms = C.c_float()
+    _check(lib().draid_ec_test_event_elapsed_ms(start, stop, C.byref(ms)), "event_elapsed_ms")
+    return float(ms.value)
+
+
+def launch_events(start: int, stop: int) -> None:
+    """The next batched launch of this thread stamps `start` and `stop` from its own dispatch
+    (no event packets around it)."""
+    lib().draid_ec_test_launch_events(start, stop)
 
 
 def last_error() -> str:
