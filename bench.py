@@ -405,6 +405,29 @@ def main() -> None:
         ec.encode(batch, sh)
         ec.reconstruct(batch, fail, sh)
 
+    verified = None
+    if not args.no_verify:
+        # before anything is timed: encode, erase the failed data strips of every stripe,
+        # reconstruct, compare
+        ec.encode(batch, sh)
+        torch.cuda.synchronize(dev)
+        good = view[:, :k].clone()
+        si = torch.arange(B, device=dev)
+        for slot in range(2):
+            idx = np.nonzero(fail_np[:, slot] != 0xFF)[0]
+            if len(idx):
+                ii = torch.from_numpy(idx).to(dev)
+                view[si[ii], torch.from_numpy(fail_np[idx, slot].astype(np.int64)).to(dev)] = 0
+        ec.reconstruct(batch, fail, sh)
+        torch.cuda.synchronize(dev)
+        verified = bool(torch.equal(view[:, :k], good))
+        del good
+        if world > 1:  # every rank's shard must come back
+            vt = torch.tensor([1.0 if verified else 0.0], dtype=torch.float64,
+                              device=dev if args.dist_backend == "nccl" else torch.device("cpu"))
+            dist.all_reduce(vt, op=dist.ReduceOp.MIN)
+            verified = bool(vt.item() == 1.0)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -461,26 +484,6 @@ def main() -> None:
     units = 2.0 * k * S * B * args.steps  # user-data bytes through both passes
     elapsed, units = reduce_timing(elapsed, units,
                                    dev if args.dist_backend == "nccl" else torch.device("cpu"))
-
-    verified = None
-    if not args.no_verify:
-        # erase the two failed data strips of every stripe, reconstruct, compare
-        good = view[:, :k].clone()
-        si = torch.arange(B, device=dev)
-        for slot in range(2):
-            idx = np.nonzero(fail_np[:, slot] != 0xFF)[0]
-            if len(idx):
-                ii = torch.from_numpy(idx).to(dev)
-                view[si[ii], torch.from_numpy(fail_np[idx, slot].astype(np.int64)).to(dev)] = 0
-        ec.reconstruct(batch, fail, sh)
-        torch.cuda.synchronize(dev)
-        verified = bool(torch.equal(view[:, :k], good))
-        del good
-        if world > 1:  # every rank's shard must come back
-            vt = torch.tensor([1.0 if verified else 0.0], dtype=torch.float64,
-                              device=dev if args.dist_backend == "nccl" else torch.device("cpu"))
-            dist.all_reduce(vt, op=dist.ReduceOp.MIN)
-            verified = bool(vt.item() == 1.0)
 
     value = units / elapsed / GIB
     workload = args.config
