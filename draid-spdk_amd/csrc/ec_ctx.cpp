@@ -164,9 +164,12 @@ struct Slot {
     void* host_dev = nullptr;  // the device's address of `host`
     void* dev = nullptr;
     size_t cap = 0;
-    hipEvent_t done = nullptr;      // the piece's kernel finished (slot reusable)
+    hipEvent_t done = nullptr;      // an event of this slot's own
+    hipEvent_t wait = nullptr;      // recorded behind the slot's latest kernel: `done`, or
+                                    // the event one flush shares (record_launched)
     hipEvent_t uploaded = nullptr;  // the piece's descriptors are on the device
     bool used = false;
+    bool unrecorded = false;        // launched, no event recorded behind it yet
     bool staged = false;            // holds a piece that has not launched yet: not to be reused
 };
 
@@ -184,6 +187,7 @@ struct draid_ec_ctx {
     std::deque<Group> groups;  // deque: groups never move (pinned storage, events)
     Slot slots[kSlots];
     int next = 0;
+    std::vector<int> unrecorded;  // slots launched since the last event record (record_launched)
     int staged_slots = 0;    // slots holding uploaded pieces that wait for their launch
     bool stage_ahead = true; // DRAID_EC_CTX_STAGE_AHEAD=0 turns the early uploads off (A/B, tests)
     size_t inplace_limit = kInplaceLimit;  // DRAID_EC_CTX_INPLACE_LIMIT (A/B, tests; 0: never)
@@ -594,6 +598,29 @@ void drop_staged(draid_ec_ctx* c, Group& g, size_t keep)
     g.tail_bytes = tail;
 }
 
+// One event for all the pieces launched since the last one: a record between two
+// kernels costs the stream 3-4 us, so a flush records once behind its last piece, not
+// behind each, and a ticketed flush lets the ticket's event serve (`shared`, which the
+// caller has just recorded).  The slots wait on that event before they are used again.
+int record_launched(draid_ec_ctx* c, hipEvent_t shared)
+{
+    if (c->unrecorded.empty())
+        return 0;
+    hipEvent_t ev = shared;
+    if (!ev) {
+        ev = c->slots[c->unrecorded.back()].done;
+        const hipError_t e = hipEventRecord(ev, c->stream);
+        if (e != hipSuccess)
+            return ctx_fail(e, "hipEventRecord(slots)");
+    }
+    for (int si : c->unrecorded) {
+        c->slots[si].wait = ev;
+        c->slots[si].unrecorded = false;
+    }
+    c->unrecorded.clear();
+    return 0;
+}
+
 // First half of a launch over segments [s0, s1) of a group: pack their
 // descriptors into the next pinned ring slot and DMA them on the copy stream.
 // `perm` (may be null): segment i of the group is g's segment perm[i].
@@ -647,13 +674,18 @@ int stage_piece(draid_ec_ctx* c, Group& g, const uint32_t* perm, size_t s0, size
     Slot& sl = c->slots[si];
     hipError_t e;
     if (sl.used) {  // back-pressure: the slot's previous upload+launch must be done
+        if (sl.unrecorded) {  // launched in this very batch: its event is still to come
+            const int rc = record_launched(c, nullptr);
+            if (rc)
+                return rc;
+        }
         if (ahead) {
-            if ((e = hipEventQuery(sl.done)) == hipErrorNotReady) {
+            if ((e = hipEventQuery(sl.wait)) == hipErrorNotReady) {
                 (void)hipGetLastError();
                 return kSlotBusy;
             }
         } else {
-            e = hipEventSynchronize(sl.done);
+            e = hipEventSynchronize(sl.wait);
         }
         if (e != hipSuccess)
             return ctx_fail(e, "hipEventSynchronize(slot)");
@@ -771,9 +803,11 @@ int launch_piece(draid_ec_ctx* c, Group& g, const Staged& st)
                                       st.nwork, c->stream);
     if (e != hipSuccess)
         return ctx_fail(e, "launch (segment work list)");
-    if ((e = hipEventRecord(sl.done, c->stream)) != hipSuccess)
-        return ctx_fail(e, "hipEventRecord(slot)");
     sl.used = true;
+    if (!sl.unrecorded) {
+        sl.unrecorded = true;
+        c->unrecorded.push_back(st.slot);
+    }
     return 0;
 }
 
@@ -1078,10 +1112,10 @@ int draid_ec_ctx_update_sg(draid_ec_ctx* c, uint32_t k, uint32_t m, uint32_t nd,
     return walk(c, 2, 2 * nd, m, lists, cnts, nullptr, len, exps, nd);
 }
 
-int draid_ec_ctx_flush(draid_ec_ctx* c)
+// record: one event behind everything this flush launched (false: the caller records
+// one of its own and hands it to record_launched).
+static int flush_all(draid_ec_ctx* c, bool record)
 {
-    if (!c)
-        return ctx_arg("ctx is NULL");
     DeviceGuard on(c->device);
     // Groups launch level by level (draid_ec_ctx_fence), and within a level in
     // the order their first segment of this batch was queued (a group object
@@ -1110,7 +1144,19 @@ int draid_ec_ctx_flush(draid_ec_ctx* c)
     recount(c);  // on failure: exactly the segments that did not launch
     c->level = 0;
     ++c->flushes;
+    if (record || rc) {
+        const int rr = record_launched(c, nullptr);
+        if (rc == 0)
+            rc = rr;
+    }
     return rc;
+}
+
+int draid_ec_ctx_flush(draid_ec_ctx* c)
+{
+    if (!c)
+        return ctx_arg("ctx is NULL");
+    return flush_all(c, true);
 }
 
 int draid_ec_ctx_flush_ticket(draid_ec_ctx* c, uint64_t* ticket)
@@ -1118,7 +1164,7 @@ int draid_ec_ctx_flush_ticket(draid_ec_ctx* c, uint64_t* ticket)
     if (!c || !ticket)
         return ctx_arg("flush_ticket needs a ctx and a ticket pointer");
     *ticket = 0;
-    const int rc = draid_ec_ctx_flush(c);
+    const int rc = flush_all(c, false);
     if (rc)
         return rc;
     DeviceGuard on(c->device);
@@ -1126,12 +1172,21 @@ int draid_ec_ctx_flush_ticket(draid_ec_ctx* c, uint64_t* ticket)
     hipError_t e;
     if (t - c->ticket_done > draid_ec_ctx::kTickets) {  // the event slot is still in use
         const uint64_t old = t - draid_ec_ctx::kTickets;
-        if ((e = hipEventSynchronize(c->ticket_ev[old % draid_ec_ctx::kTickets])) != hipSuccess)
+        if ((e = hipEventSynchronize(c->ticket_ev[old % draid_ec_ctx::kTickets])) != hipSuccess) {
+            (void)record_launched(c, nullptr);
             return ctx_fail(e, "hipEventSynchronize(ticket)");
+        }
         c->ticket_done = old;
     }
-    if ((e = hipEventRecord(c->ticket_ev[t % draid_ec_ctx::kTickets], c->stream)) != hipSuccess)
+    hipEvent_t tev = c->ticket_ev[t % draid_ec_ctx::kTickets];
+    if ((e = hipEventRecord(tev, c->stream)) != hipSuccess) {
+        (void)record_launched(c, nullptr);
         return ctx_fail(e, "hipEventRecord(ticket)");
+    }
+    // the ticket's event also tells when this flush's ring slots are free again (a slot
+    // is used again 16 launches later at the earliest, the event 64 tickets later: were
+    // it recorded again by then, the slot would wait for a later flush, never a shorter time)
+    (void)record_launched(c, tev);
     c->ticket_next = t + 1;
     *ticket = t;
     return 0;
