@@ -348,3 +348,44 @@ def test_early_uploads_leave_slots_for_other_groups(ec):
         assert (d2.cpu().numpy() == ref2).all()
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("ahead", [True, False])
+def test_one_flush_of_more_pieces_than_ring_slots(ec, ahead, monkeypatch):
+    """A context records one event per flush, behind its last piece, and its sixteen ring
+    slots wait on that event before they are used again.  A single batch of eighteen pieces
+    comes round to slots of its own earlier pieces: those must get their event first.
+    (ahead: up to twelve of the pieces are uploaded from inside the queueing calls; not
+    ahead: the flush packs all of them itself.)  Then a second batch on the same context."""
+    if not ahead:
+        monkeypatch.setenv("DRAID_EC_CTX_STAGE_AHEAD", "0")
+    k, m, L = 20, 2, 32
+    n = k + m
+    piece = _piece(k, m)
+    B = 17 * piece + 333
+    a, ref = stripes(k, m, L, B, 23)
+    d = torch.from_numpy(a).to(DEV)
+    base = d.data_ptr()
+    torch.cuda.synchronize()
+    ctx = ec.Ctx()
+    try:
+        for rnd in range(2):
+            if rnd:
+                d[:, k:].zero_()
+                torch.cuda.synchronize()
+            for s in range(B):
+                ctx.encode_sg(k, m, [[(base + (s * n + j) * L, L)] for j in range(n)], L)
+            assert ctx.queued() == B
+            if rnd == 0:
+                ctx.flush()
+            else:
+                t = ctx.flush_ticket()
+            ctx.synchronize()
+            if rnd:
+                assert ctx.ticket_query(t) == 0
+            assert ctx.queued() == 0 and ctx.test_staged() == 0
+            got = d.cpu().numpy()
+            bad = np.nonzero((got != ref).any(axis=(1, 2)))[0]
+            assert bad.size == 0, (rnd, bad[:8])
+    finally:
+        ctx.close()
