@@ -24,6 +24,10 @@ timeout -k 10 120 tests/c/sg_bench_asan_gpu 4096 512 3 0 1024 >> $L 2>&1 || { ta
 # batch at 1 KiB iovecs x 1024 stripes), alone and with autoflush launching between them
 timeout -k 10 180 tests/c/sg_bench_asan_gpu 1024 1024 2 0 >> $L 2>&1 || { tail -40 $L; exit 1; }
 timeout -k 10 180 tests/c/sg_bench_asan_gpu 1024 1024 2 0 30000 >> $L 2>&1 || { tail -40 $L; exit 1; }
+# one batch of more descriptor pieces than the context has ring slots (28 over 16): slots of
+# the batch's own earlier pieces are waited for and used again inside the one flush
+DRAID_EC_CTX_STAGE_AHEAD=0 timeout -k 10 240 tests/c/sg_bench_asan_gpu 1024 8192 1 0 >> $L 2>&1 || { tail -40 $L; exit 1; }
+timeout -k 10 240 tests/c/sg_bench_asan_gpu 1024 8192 1 0 >> $L 2>&1 || { tail -40 $L; exit 1; }
 # pageable memory: the pinned bounce arena and the device arena of the isa-l-shaped calls,
 # and host stripes bounced through pinned buffers by the calling thread
 timeout -k 10 300 tests/c/test_pageable_asan_gpu >> $L 2>&1 || { tail -40 $L; exit 1; }
