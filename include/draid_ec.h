@@ -272,9 +272,10 @@ int draid_ec_ctx_ticket_query(draid_ec_ctx *ctx, uint64_t ticket);
  * pointer -- and is resolved to its device address while the descriptors are
  * written (draid_ec_device_pointer's cached lookup, one per iovec).  A stripe
  * with an iovec the GPU cannot reach is rejected with 1 and queues nothing.
- * The context then also knows which segments lie in host memory, and launches
- * small batches of those with fewer workgroups resident per CU (a PCIe-bound
- * launch of a few dozen stripes is 14-18% faster that way).  Off by default. */
+ * The context then also knows which segments lie in host memory, and runs
+ * batches of those in kernels that loop over the work items with one workgroup
+ * per CU (a PCIe-bound launch of a few dozen stripes is 11-13% faster that way
+ * than with a workgroup per item, a large one 3%).  Off by default. */
 int draid_ec_ctx_set_host_pointers(draid_ec_ctx *ctx, int on);
 int draid_ec_ctx_query(draid_ec_ctx *ctx);
 int draid_ec_ctx_synchronize(draid_ec_ctx *ctx);
